@@ -1,0 +1,138 @@
+/*
+ * mxmoe_gg.h — C-ABI of the MI355X (gfx950) mixed-precision MoE GroupGEMM.
+ *
+ * One call computes P independent problems  C_i[M_i,N_i] = A_i[M_i,K_i] . B_i[N_i,K_i]^T
+ * (RCR layout: A row-major, B "column-major" = [N][K] with K contiguous, C row-major fp16),
+ * each problem with its own quantisation type:
+ *
+ *   fp16 : A,B fp16, fp32 accumulate, C = fp16_rn(acc)
+ *   w8a8 : A,B int8  per-channel sym (gsize -1), exact int32 accumulate,
+ *          C = fp16_rn(0.f + f32(acc) * f32(fp16_rn(sa[m] * sb[n])))
+ *   w4a4 : A,B int4  per-channel sym (gsize -1), same epilogue
+ *
+ * Data layout is byte-identical to the reference bench (SeaCatComplexes/MxMoE):
+ *   - packed A/B words follow pack_wxax        (mxmoe/kernels/src/include/quantize.cuh:425-475)
+ *   - QParams {int2 qbits(x=a_bits,y=w_bits); int gsize; bool sym}  (quantize.cuh:14-25)
+ *   - scale_a[M], scale_b[N] fp16 per problem  (test.cu:301-313, 522-523)
+ *   - epilogue arithmetic                      (mm_tile.cuh:469-496, 610-662; cta_gemm.cuh:599-607)
+ *
+ * Conventions (differences from the reference ABI):
+ *   - every entry point returns an int status (MXMOE_GG_OK == 0); nothing calls exit();
+ *     mxmoe_gg_last_error() returns a thread-local message for the last failure;
+ *   - the caller owns all device memory, including the workspace; no call allocates
+ *     device memory except the reference-compatible shim groupgemm_mxmoe();
+ *   - explicit stream argument (hipStream_t passed as void*); mxmoe_gg_launch() does no host
+ *     synchronisation and no allocation, so it can be captured into a hipGraph;
+ *   - no mutable global state besides the thread-local error string.
+ */
+#ifndef MXMOE_GG_H_
+#define MXMOE_GG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MXMOE_GG_ABI_VERSION 1
+
+enum {
+  MXMOE_GG_OK = 0,
+  MXMOE_GG_ERR_INVALID = 1,     /* bad argument / shape / alignment */
+  MXMOE_GG_ERR_UNSUPPORTED = 2, /* quantisation type or variant not compiled */
+  MXMOE_GG_ERR_WORKSPACE = 3,   /* workspace too small */
+  MXMOE_GG_ERR_HIP = 4          /* a HIP runtime call failed */
+};
+
+/* Same memory layout as the reference's mxmoe::QParams (quantize.cuh:14-25):
+ * int2 qbits {x = a_bits, y = w_bits}; int gsize; bool sym; padded to 16 bytes, 8-byte aligned. */
+typedef struct mxmoe_qparams {
+  int32_t a_bits;
+  int32_t w_bits;
+  int32_t gsize;
+  uint8_t sym;
+  uint8_t pad_[3];
+} __attribute__((aligned(8))) mxmoe_qparams;
+
+/* Same memory layout as CUDA/HIP dim3 (x = M, y = N, z = K), as used in registry.cuh:28-39. */
+typedef struct mxmoe_dim3 {
+  uint32_t x, y, z;
+} mxmoe_dim3;
+
+/* One GroupGEMM problem (host-side descriptor). Pointers are DEVICE pointers.
+ * lda/ldb/ldc are row strides in 16-bit words (the reference's `half` unit); 0 = dense. */
+typedef struct mxmoe_gg_problem {
+  const void* A;       /* fp16 [M][K]  or packed [M][K*a_bits/16] words            */
+  const void* B;       /* fp16 [N][K]  or packed [N][K*w_bits/16] words            */
+  const void* scale_a; /* fp16 [M] (quantised problems only, else may be NULL)     */
+  const void* scale_b; /* fp16 [N] (quantised problems only, else may be NULL)     */
+  void* C;             /* fp16 [M][ldc]                                            */
+  int32_t M, N, K;
+  int32_t a_bits, w_bits, gsize, sym;
+  int32_t reserved_;
+  int64_t lda, ldb, ldc;
+} mxmoe_gg_problem;
+
+/* Result of planning: what mxmoe_gg_launch needs on the host side. */
+typedef struct mxmoe_gg_plan_info {
+  int32_t variant;
+  int32_t problem_count;
+  int32_t total_tiles;
+  int32_t grid;
+  int32_t block;
+  int32_t lds_bytes;
+  int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */
+  void* workspace;         /* device workspace the plan was written to */
+} mxmoe_gg_plan_info;
+
+int mxmoe_gg_abi_version(void);
+
+/* Thread-local message describing the last failed call on this thread ("" if none). */
+const char* mxmoe_gg_last_error(void);
+
+/* Number of compiled kernel variants. */
+int mxmoe_gg_variant_count(void);
+
+/* Writes a newline-separated description of every compiled variant into buf (truncated,
+ * always NUL-terminated when n > 0). Line i describes variant i in the reference TileConfig
+ * repr form per qcfg, e.g. "0 fused fp16=TileConfig(BM=128, BN=128, ...) w8a8_g-1_sym=...".
+ * Returns the number of variants, or a negative status on error. */
+int mxmoe_gg_list_variants(char* buf, size_t n);
+
+/* Tile geometry of variant `variant` for a quantisation type (a_bits, w_bits):
+ * writes BM, BN, K-bytes-per-stage and threads per workgroup. */
+int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int32_t* bn, int32_t* bk_bytes,
+                          int32_t* threads);
+
+/* Device workspace bytes needed for P problems. */
+int mxmoe_gg_workspace_size(int problem_count, size_t* bytes);
+
+/* Validate problems, build the tile table and upload it (hipMemcpyAsync on `stream`) into
+ * the workspace. Host problem array may be freed after return. */
+int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int variant, void* workspace,
+                  size_t workspace_bytes, void* stream, mxmoe_gg_plan_info* info);
+
+/* Launch a planned GroupGEMM on `stream`. No allocation, no synchronisation. */
+int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream);
+
+/* plan + launch. */
+int mxmoe_gg_run(const mxmoe_gg_problem* problems, int problem_count, int variant, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
+/* Drop-in for the reference registry FuncType (mxmoe/kernels/src/include/registry.cuh:28-39;
+ * generated host API groupgemm_hz_fused_<i>, kernel_sketch.py:25-46, 82-145).
+ * ptr_* / problem_sizes / qbits_list are DEVICE arrays, h_problem_sizes / h_qbits_list host
+ * copies; ptr_Ds and the ld* arrays are accepted and ignored exactly as in the reference.
+ * Runs the default variant on the legacy default stream. Unlike the reference it reports
+ * errors through the return value (and mxmoe_gg_last_error) instead of exit(). */
+int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr_scale_b, void** ptr_Cs,
+                    void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
+                    mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
+                    mxmoe_qparams* h_qbits_list, int problem_count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MXMOE_GG_H_ */

@@ -1,0 +1,150 @@
+"""ctypes binding of ``libmxmoe_gg.so`` (the C-ABI in ``include/mxmoe_gg.h``).
+
+The library is the product path: if it is missing or does not load, every GPU entry point raises
+``NativeLibraryError`` — there is no CPU or PyTorch fallback anywhere in the package.
+
+torch is imported before the library is opened so that ``libamdhip64.so.7`` resolves to the HIP
+runtime torch already loaded (one runtime per process; streams and device pointers are shared).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL: binds the shared HIP runtime)
+
+LIB_DIR = Path(__file__).resolve().parent / "lib"
+LIB_PATH = LIB_DIR / "libmxmoe_gg.so"
+
+MXMOE_GG_OK = 0
+MXMOE_GG_ERR_INVALID = 1
+MXMOE_GG_ERR_UNSUPPORTED = 2
+MXMOE_GG_ERR_WORKSPACE = 3
+MXMOE_GG_ERR_HIP = 4
+
+
+class NativeLibraryError(RuntimeError):
+    """libmxmoe_gg.so is missing or failed to load."""
+
+
+class GGError(RuntimeError):
+    """A C-ABI call returned a non-zero status."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"mxmoe_gg status {status}: {message}")
+        self.status = status
+
+
+class MxmoeQParams(ctypes.Structure):
+    """Layout of the reference's mxmoe::QParams (quantize.cuh:14-25): int2 qbits; int gsize; bool sym."""
+
+    _pack_ = 8
+    _fields_ = [("a_bits", ctypes.c_int32), ("w_bits", ctypes.c_int32), ("gsize", ctypes.c_int32),
+                ("sym", ctypes.c_uint8), ("pad_", ctypes.c_uint8 * 3)]
+
+
+class MxmoeDim3(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint32), ("y", ctypes.c_uint32), ("z", ctypes.c_uint32)]
+
+
+class GGProblemC(ctypes.Structure):
+    _fields_ = [
+        ("A", ctypes.c_void_p), ("B", ctypes.c_void_p), ("scale_a", ctypes.c_void_p),
+        ("scale_b", ctypes.c_void_p), ("C", ctypes.c_void_p),
+        ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
+        ("a_bits", ctypes.c_int32), ("w_bits", ctypes.c_int32), ("gsize", ctypes.c_int32),
+        ("sym", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+        ("lda", ctypes.c_int64), ("ldb", ctypes.c_int64), ("ldc", ctypes.c_int64),
+    ]
+
+
+class GGPlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("variant", ctypes.c_int32), ("problem_count", ctypes.c_int32), ("total_tiles", ctypes.c_int32),
+        ("grid", ctypes.c_int32), ("block", ctypes.c_int32), ("lds_bytes", ctypes.c_int32),
+        ("workspace_bytes", ctypes.c_int64), ("workspace", ctypes.c_void_p),
+    ]
+
+
+# every symbol include/mxmoe_gg.h declares (tests check the .so exports exactly these)
+EXPORTED_SYMBOLS = (
+    "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_list_variants",
+    "mxmoe_gg_variant_tile", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
+    "groupgemm_mxmoe",
+)
+
+_lib = None
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    c = ctypes
+    lib.mxmoe_gg_abi_version.restype = c.c_int
+    lib.mxmoe_gg_abi_version.argtypes = []
+    lib.mxmoe_gg_last_error.restype = c.c_char_p
+    lib.mxmoe_gg_last_error.argtypes = []
+    lib.mxmoe_gg_variant_count.restype = c.c_int
+    lib.mxmoe_gg_variant_count.argtypes = []
+    lib.mxmoe_gg_list_variants.restype = c.c_int
+    lib.mxmoe_gg_list_variants.argtypes = [c.c_char_p, c.c_size_t]
+    lib.mxmoe_gg_variant_tile.restype = c.c_int
+    lib.mxmoe_gg_variant_tile.argtypes = [c.c_int, c.c_int, c.c_int] + [c.POINTER(c.c_int32)] * 4
+    lib.mxmoe_gg_workspace_size.restype = c.c_int
+    lib.mxmoe_gg_workspace_size.argtypes = [c.c_int, c.POINTER(c.c_size_t)]
+    lib.mxmoe_gg_plan.restype = c.c_int
+    lib.mxmoe_gg_plan.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
+                                  c.POINTER(GGPlanInfo)]
+    lib.mxmoe_gg_launch.restype = c.c_int
+    lib.mxmoe_gg_launch.argtypes = [c.POINTER(GGPlanInfo), c.c_void_p]
+    lib.mxmoe_gg_run.restype = c.c_int
+    lib.mxmoe_gg_run.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.groupgemm_mxmoe.restype = c.c_int
+    lib.groupgemm_mxmoe.argtypes = [c.c_void_p] * 10 + [c.c_void_p, c.POINTER(MxmoeDim3), c.c_void_p,
+                                                         c.POINTER(MxmoeQParams), c.c_int]
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library; raises NativeLibraryError (never falls back)."""
+    global _lib
+    if _lib is None:
+        path = Path(os.environ.get("MXMOE_GG_LIB", LIB_PATH))
+        if not path.exists():
+            raise NativeLibraryError(
+                f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). There is no fallback path.")
+        try:
+            _lib = ctypes.CDLL(str(path))
+        except OSError as e:  # pragma: no cover - environment dependent
+            raise NativeLibraryError(f"failed to load {path}: {e}") from e
+        _declare(_lib)
+    return _lib
+
+
+def check(status: int) -> None:
+    if status != MXMOE_GG_OK:
+        msg = lib().mxmoe_gg_last_error().decode(errors="replace")
+        raise GGError(status, msg)
+
+
+def variant_count() -> int:
+    return lib().mxmoe_gg_variant_count()
+
+
+def list_variants() -> list[str]:
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = lib().mxmoe_gg_list_variants(buf, len(buf))
+    if n < 0:
+        check(-n)
+    return [ln for ln in buf.value.decode().splitlines() if ln]
+
+
+def variant_tile(variant: int, a_bits: int, w_bits: int) -> dict:
+    v = [ctypes.c_int32() for _ in range(4)]
+    check(lib().mxmoe_gg_variant_tile(variant, a_bits, w_bits, *[ctypes.byref(x) for x in v]))
+    return {"BM": v[0].value, "BN": v[1].value, "BK_bytes": v[2].value, "threads": v[3].value}
+
+
+def workspace_size(problem_count: int) -> int:
+    n = ctypes.c_size_t()
+    check(lib().mxmoe_gg_workspace_size(problem_count, ctypes.byref(n)))
+    return n.value

@@ -1,0 +1,44 @@
+"""Build libmxmoe_gg.so in-tree with hipcc for gfx950 (no JIT cache: the .so travels with the repo)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "lib" / "libmxmoe_gg.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("MXMOE_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = [CSRC / "gg_api.hip"]
+DEPS = SOURCES + [CSRC / "gg_device.h", ROOT / "include" / "mxmoe_gg.h"]
+
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-I", str(ROOT / "include")]
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None) -> Path:
+    if not force and not needs_build():
+        return LIB
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, *FLAGS, *(extra or []), "-o", str(tmp), *map(str, SOURCES)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

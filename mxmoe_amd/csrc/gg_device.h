@@ -1,0 +1,337 @@
+// gg_device.h — device side of the MI355X (gfx950) fused mixed-precision GroupGEMM.
+//
+// What the reference does (SeaCatComplexes/MxMoE, read as text only):
+//   persistent fused kernel, per-tile qtype branch ........ compose_kernel.py:150-224, generated/hz_fused_0.cu:12-97
+//   tile -> (problem, m-tile, n-tile), n fastest .......... tile_scheduler.cuh:25-50
+//   fp16 mainloop (fp32 acc) .............................. cta_gemm.cuh:7-107
+//   w8a8 / w4a4 mainloop (exact int32 acc) + epilogue ..... cta_gemm.cuh:423-608
+//   epilogue  out = fp16_rn(0 + f32(acc) * f32(fp16_rn(sa*sb))) ... mm_tile.cuh:469-496, 610-662
+//
+// How it is built here (MI355X-first, not a translation):
+//   * one workgroup per output tile, grid = #tiles, XCD-aware bijective blockIdx remap;
+//     tile -> problem by binary search over the tile-begin column of the plan table;
+//   * K staged 128 BYTES per stage for every dtype (64 fp16 / 128 int8 / 256 int4 elements),
+//     global -> registers (16 B per lane, coalesced 128-B row segments) -> LDS, double buffered,
+//     one barrier per stage; LDS rows are 128 B with a (row>>1)&7 XOR swizzle of the 16-B chunk,
+//     which makes both the 8-lane row writes and the 16-row ds_read_b128 / ds_read_b64 fragment
+//     reads bank-conflict free;
+//   * MFMA: v_mfma_i32_16x16x64_i8 for w8a8 AND w4a4 (int4 nibbles are widened in registers to
+//     16*q int8 values: hi = w & 0xF0F0F0F0, lo = (w << 4) & 0xF0F0F0F0, so the int32 sum is
+//     exactly 256 * sum(a*b) and one arithmetic shift restores it: bit-exact), and
+//     v_mfma_f32_16x16x32_f16 for fp16.  A and B fragments use the SAME K->(lane group, element)
+//     assignment, so the (unspecified) K order inside an MFMA and the pack_wxax K permutation
+//     (quantize.cuh:425-475) cancel: every product a[m,k]*b[n,k] is formed exactly once;
+//   * epilogue: scale in registers, fp16 tile staged through LDS, 16-B coalesced row stores.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mxmoe {
+
+enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_COUNT = 3 };
+
+// One row of the plan table (64 B), written by the host planner into the workspace.
+struct GGMeta {
+  int32_t M, N, K, qtype;
+  int32_t tiles_n;     // cdiv(N, BN of this qtype)
+  int32_t tile_begin;  // first global tile id of this problem
+  int32_t kbytes;      // bytes of one K row (K * bits / 8)
+  int32_t reserved;
+  int64_t lda_b, ldb_b;  // row strides of A / B in bytes
+  int64_t ldc;           // row stride of C in fp16 elements
+  int64_t reserved2;
+};
+static_assert(sizeof(GGMeta) == 64, "GGMeta must stay 64 bytes");
+
+struct GGArgs {
+  const GGMeta* meta;
+  const void* const* ptr_A;
+  const void* const* ptr_B;
+  const void* const* ptr_SA;
+  const void* const* ptr_SB;
+  void* const* ptr_C;
+  int32_t P;
+  int32_t total_tiles;
+};
+
+typedef int32_t v2i __attribute__((ext_vector_type(2)));
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+
+// Compile-time tile geometry. All dtypes stage 128 bytes of K per stage.
+template <int BM_, int BN_, int WM_, int WN_, int MIN_WAVES_PER_EU_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int kThreads = WM * WN * 64;
+  static constexpr int kMinWavesPerEU = MIN_WAVES_PER_EU_;
+  static constexpr int BKB = 128;  // bytes of K per stage
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB;
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int C_STRIDE = BN + 8;  // fp16 elements per staged C row (pad: spreads banks)
+  static constexpr int C_BYTES = BM * C_STRIDE * 2;
+  static constexpr int LDS_BYTES = (2 * STAGE_BYTES > C_BYTES) ? 2 * STAGE_BYTES : C_BYTES;
+  static constexpr int LA = BM * 8 / kThreads;  // 16-B chunks per thread per stage (A)
+  static constexpr int LB = BN * 8 / kThreads;  // (B)
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile must be a multiple of 16");
+  static_assert((BM * 8) % kThreads == 0 && (BN * 8) % kThreads == 0, "stage chunks must divide threads");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+// 16-B chunk `chunk` (0..7) of LDS row `row` (128-B rows), XOR-swizzled.
+__device__ __forceinline__ uint32_t lds_off(int row, int chunk) {
+  return (uint32_t)(row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+}
+
+// Bijective XCD-aware remap: blocks b and b+8 share an XCD under round-robin dispatch, so give
+// each group of blocks {x, x+8, x+16, ...} a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7;
+  const int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + (b >> 3);
+}
+
+// Widen 8 packed int4 (two's complement nibbles) per dword to int8 lanes holding 16*q.
+__device__ __forceinline__ v4i widen_i4(v2i w) {
+  const int32_t m = (int32_t)0xF0F0F0F0u;
+  v4i r;
+  r.x = w.x & m;
+  r.y = (w.x << 4) & m;
+  r.z = w.y & m;
+  r.w = (w.y << 4) & m;
+  return r;
+}
+
+template <int QT>
+struct AccT {
+  typedef v4i type;
+};
+template <>
+struct AccT<QT_F16> {
+  typedef v4f type;
+};
+
+// One output tile of one problem.
+template <class Cfg, int QT>
+__device__ __forceinline__ void gg_tile(const GGMeta& mt, const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                        const _Float16* __restrict__ SA, const _Float16* __restrict__ SB,
+                                        _Float16* __restrict__ C, int m_tile, int n_tile, uint8_t* lds) {
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, NT = Cfg::kThreads;
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, LA = Cfg::LA, LB = Cfg::LB;
+  typedef typename AccT<QT>::type acc_t;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int rows_a = min(BM, mt.M - m0);
+  const int rows_b = min(BN, mt.N - n0);
+  const int kbytes = mt.kbytes;
+  const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
+  const uint8_t* Ablk = A + (int64_t)m0 * lda;
+  const uint8_t* Bblk = B + (int64_t)n0 * ldb;
+  const int nstage = (kbytes + Cfg::BKB - 1) / Cfg::BKB;
+
+  uint4 ra[LA], rb[LB];
+  acc_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+
+  auto gload = [&](int s) {
+    const int kb = s * Cfg::BKB;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int q = tid + i * NT, row = q >> 3, c = q & 7;
+      const bool p = (row < rows_a) && (kb + c * 16 < kbytes);
+      ra[i] = p ? *reinterpret_cast<const uint4*>(Ablk + (int64_t)row * lda + kb + c * 16) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int q = tid + i * NT, row = q >> 3, c = q & 7;
+      const bool p = (row < rows_b) && (kb + c * 16 < kbytes);
+      rb[i] = p ? *reinterpret_cast<const uint4*>(Bblk + (int64_t)row * ldb + kb + c * 16) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto swrite = [&](int buf) {
+    uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
+    uint8_t* Bs = As + Cfg::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int q = tid + i * NT;
+      *reinterpret_cast<uint4*>(As + lds_off(q >> 3, q & 7)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int q = tid + i * NT;
+      *reinterpret_cast<uint4*>(Bs + lds_off(q >> 3, q & 7)) = rb[i];
+    }
+  };
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
+    const uint8_t* Bs = As + Cfg::A_BYTES;
+    const int r16 = lane & 15, g = lane >> 4;
+    if constexpr (QT == QT_I4) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {  // 4 x 32 bytes (= 64 int4) per 128-B stage
+        v4i a[FM], b[FN];
+        const int chunk = 2 * s + (g >> 1), half = (g & 1) * 8;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * Cfg::WTM + i * 16 + r16;
+          a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + lds_off(row, chunk) + half));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * Cfg::WTN + j * 16 + r16;
+          b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + lds_off(row, chunk) + half));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {  // 2 x 64 bytes per 128-B stage
+        const int chunk = kc * 4 + g;
+        if constexpr (QT == QT_I8) {
+          v4i a[FM], b[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            a[i] = *reinterpret_cast<const v4i*>(As + lds_off(wm * Cfg::WTM + i * 16 + r16, chunk));
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            b[j] = *reinterpret_cast<const v4i*>(Bs + lds_off(wn * Cfg::WTN + j * 16 + r16, chunk));
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+        } else {
+          v8h a[FM], b[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            a[i] = *reinterpret_cast<const v8h*>(As + lds_off(wm * Cfg::WTM + i * 16 + r16, chunk));
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            b[j] = *reinterpret_cast<const v8h*>(Bs + lds_off(wn * Cfg::WTN + j * 16 + r16, chunk));
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- mainloop: register-staged double buffer, one barrier per stage ----
+  if (nstage > 0) {
+    gload(0);
+    swrite(0);
+    __syncthreads();
+    for (int s = 0; s < nstage; ++s) {
+      const bool more = (s + 1) < nstage;
+      if (more) gload(s + 1);
+      compute(s & 1);
+      if (more) swrite((s + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: scale (quant) / round, stage the fp16 tile in LDS, coalesced 16-B stores ----
+  _Float16* Cs = reinterpret_cast<_Float16*>(lds);
+  const int r16 = lane & 15, g = lane >> 4;
+  if constexpr (QT == QT_F16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = wm * Cfg::WTM + i * 16 + 4 * g + r, lc = wn * Cfg::WTN + j * 16 + r16;
+          Cs[lr * Cfg::C_STRIDE + lc] = (_Float16)acc[i][j][r];
+        }
+  } else {
+    constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
+    _Float16 sb[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int lc = wn * Cfg::WTN + j * 16 + r16;
+      sb[j] = (lc < rows_b) ? SB[n0 + lc] : (_Float16)0;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wm * Cfg::WTM + i * 16 + 4 * g + r;
+        const _Float16 sa = (lr < rows_a) ? SA[m0 + lr] : (_Float16)0;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int lc = wn * Cfg::WTN + j * 16 + r16;
+          const _Float16 s16 = sa * sb[j];  // fp16 product, RN (mm_tile.cuh:490-493)
+          const float v = 0.0f + (float)(acc[i][j][r] >> SHIFT) * (float)s16;
+          Cs[lr * Cfg::C_STRIDE + lc] = (_Float16)v;
+        }
+      }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16-B chunks per C row
+#pragma unroll 4
+  for (int q = tid; q < BM * CPR; q += NT) {
+    const int row = q / CPR, c = q % CPR;
+    if (row < rows_a && c * 8 < rows_b) {
+      const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * Cfg::C_STRIDE + c * 8);
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + row) * mt.ldc + n0 + c * 8) = v;
+    }
+  }
+  __syncthreads();  // LDS is reused by the next tile of a persistent caller
+}
+
+template <class C16, class C8, class C4>
+struct FusedCfg {
+  static_assert(C16::kThreads == C8::kThreads && C8::kThreads == C4::kThreads,
+                "fused tiles must use the same workgroup size (compose_kernel.py:69-71)");
+  static constexpr int kThreads = C16::kThreads;
+  static constexpr int kMinWavesPerEU = C16::kMinWavesPerEU;
+  static constexpr int m1 = C16::LDS_BYTES > C8::LDS_BYTES ? C16::LDS_BYTES : C8::LDS_BYTES;
+  static constexpr int LDS_BYTES = m1 > C4::LDS_BYTES ? m1 : C4::LDS_BYTES;
+};
+
+// Fused GroupGEMM: one workgroup per tile; the qtype branch is uniform per workgroup.
+template <class C16, class C8, class C4>
+__global__ __launch_bounds__(C16::kThreads, C16::kMinWavesPerEU) void gg_fused_kernel(GGArgs args) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[FusedCfg<C16, C8, C4>::LDS_BYTES];
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t >= args.total_tiles) return;
+  // binary search: last problem with tile_begin <= t (empty problems are never planned)
+  int lo = 0, hi = args.P - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (args.meta[mid].tile_begin <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const GGMeta mt = args.meta[lo];
+  const int local = t - mt.tile_begin;
+  const int m_tile = local / mt.tiles_n, n_tile = local - m_tile * mt.tiles_n;
+  const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[lo]);
+  const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[lo]);
+  _Float16* C = static_cast<_Float16*>(args.ptr_C[lo]);
+  if (mt.qtype == QT_I8) {
+    gg_tile<C8, QT_I8>(mt, A, B, static_cast<const _Float16*>(args.ptr_SA[lo]),
+                       static_cast<const _Float16*>(args.ptr_SB[lo]), C, m_tile, n_tile, lds);
+  } else if (mt.qtype == QT_I4) {
+    gg_tile<C4, QT_I4>(mt, A, B, static_cast<const _Float16*>(args.ptr_SA[lo]),
+                       static_cast<const _Float16*>(args.ptr_SB[lo]), C, m_tile, n_tile, lds);
+  } else {
+    gg_tile<C16, QT_F16>(mt, A, B, nullptr, nullptr, C, m_tile, n_tile, lds);
+  }
+}
+
+}  // namespace mxmoe

@@ -1,0 +1,165 @@
+"""Host-side mirror of the reference GroupGEMM operator interface, on the HIP C-ABI.
+
+Reference interface mirrored (SeaCatComplexes/MxMoE):
+  * per-problem QParams {qbits=(a_bits, w_bits), gsize, sym} ..... quantize.cuh:14-25
+  * the host API groupgemm_hz_fused_<i>(ptr_As, ptr_Bs, ptr_scale_a, ptr_scale_b, ptr_Cs, ...,
+    problem_sizes, qbits_list, problem_count) ...................... kernel_sketch.py:25-46, 82-145
+  * the kernel registry (name -> FuncType), registry.cuh:72-107 .... ``registry()``
+  * "quant type not supported" for an uncompiled qcfg .............. compose_kernel.py:433
+
+Differences by design: the tile table is planned once into a caller-owned device workspace
+(``GroupGemm``), launches are allocation/sync free and run on the caller's stream (torch's
+current stream by default), and errors raise ``GGError`` instead of exiting the process.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native as nat
+
+
+@dataclasses.dataclass(frozen=True)
+class QParams:
+    """Per-problem quantisation parameters (reference QParams, quantize.cuh:14-25)."""
+
+    a_bits: int = 16
+    w_bits: int = 16
+    gsize: int = -1
+    sym: bool = True
+
+    @property
+    def is_quant(self) -> bool:
+        return self.a_bits < 16 or self.w_bits < 16
+
+    @property
+    def qcfg(self) -> str:
+        if not self.is_quant:
+            return "fp16"
+        return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}"
+
+    @staticmethod
+    def from_qcfg(qcfg: str) -> "QParams":
+        if qcfg in ("fp16",):
+            return QParams()
+        w = int(qcfg.split("w")[1].split("a")[0])
+        a = int(qcfg.split("a")[1].split("_g")[0])
+        g = int(qcfg.split("_g")[1].split("_")[0])
+        return QParams(a_bits=a, w_bits=w, gsize=g, sym="asym" not in qcfg)
+
+
+FP16 = QParams()
+W8A8 = QParams(8, 8, -1, True)
+W4A4 = QParams(4, 4, -1, True)
+
+SUPPORTED = {FP16.qcfg: FP16, W8A8.qcfg: W8A8, W4A4.qcfg: W4A4}
+
+
+@dataclasses.dataclass
+class Problem:
+    """One GroupGEMM problem  C[M,N] = A[M,K] . B[N,K]^T  on device tensors.
+
+    fp16: A fp16 [M,K], B fp16 [N,K].  quant: A uint8 [M, K*a_bits/8] / B uint8 [N, K*w_bits/8]
+    in pack_wxax layout, scale_a fp16 [M], scale_b fp16 [N].  C fp16 [M, ldc] (ldc >= N).
+    """
+
+    A: torch.Tensor
+    B: torch.Tensor
+    C: torch.Tensor
+    M: int
+    N: int
+    K: int
+    q: QParams = FP16
+    scale_a: Optional[torch.Tensor] = None
+    scale_b: Optional[torch.Tensor] = None
+    lda: int = 0  # row strides in 16-bit words, 0 = dense
+    ldb: int = 0
+    ldc: int = 0
+
+    def to_c(self) -> nat.GGProblemC:
+        def ptr(t):
+            return 0 if t is None else t.data_ptr()
+
+        return nat.GGProblemC(
+            A=ptr(self.A), B=ptr(self.B), scale_a=ptr(self.scale_a), scale_b=ptr(self.scale_b), C=ptr(self.C),
+            M=self.M, N=self.N, K=self.K, a_bits=self.q.a_bits, w_bits=self.q.w_bits, gsize=self.q.gsize,
+            sym=int(self.q.sym), reserved_=0, lda=self.lda, ldb=self.ldb, ldc=self.ldc)
+
+    @property
+    def flops(self) -> int:
+        return 2 * self.M * self.N * self.K
+
+
+def registry() -> list[str]:
+    """Compiled kernel variants (the reference's GetGlobalRegistry(), registry.cuh:99-102)."""
+    return nat.list_variants()
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+class GroupGemm:
+    """A planned GroupGEMM: the tile table lives in a device workspace owned by this object.
+
+    ``launch()`` is a single kernel launch on the given (or current) stream; it performs no
+    allocation and no host synchronisation, so it can be captured in a CUDA/HIP graph.
+    """
+
+    def __init__(self, problems: Sequence[Problem], variant: int = 0, device: Optional[torch.device] = None,
+                 stream: Optional[torch.cuda.Stream] = None):
+        self.problems = list(problems)
+        self.variant = int(variant)
+        if device is None:
+            device = self.problems[0].C.device if self.problems else torch.device("cuda")
+        self.device = device
+        for p in self.problems:
+            for t in (p.A, p.B, p.C, p.scale_a, p.scale_b):
+                if t is not None and t.device != device:
+                    raise ValueError(f"all tensors must live on {device}, got {t.device}")
+        P = len(self.problems)
+        self._c_problems = (nat.GGProblemC * max(P, 1))(*[p.to_c() for p in self.problems])
+        ws_bytes = nat.workspace_size(P)
+        self.workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+        self.info = nat.GGPlanInfo()
+        nat.check(nat.lib().mxmoe_gg_plan(self._c_problems, P, self.variant, ctypes.c_void_p(self.workspace.data_ptr()),
+                                          ws_bytes, ctypes.c_void_p(_stream_handle(stream)), ctypes.byref(self.info)))
+
+    @property
+    def total_tiles(self) -> int:
+        return self.info.total_tiles
+
+    @property
+    def flops(self) -> int:
+        return sum(p.flops for p in self.problems)
+
+    def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        nat.check(nat.lib().mxmoe_gg_launch(ctypes.byref(self.info), ctypes.c_void_p(_stream_handle(stream))))
+
+    __call__ = launch
+
+
+def group_gemm(problems: Sequence[Problem], variant: int = 0, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Plan + launch once (the reference host API's per-call behaviour)."""
+    GroupGemm(problems, variant=variant, stream=stream).launch(stream)
+
+
+def groupgemm_reference_abi(ptr_As: torch.Tensor, ptr_Bs: torch.Tensor, ptr_scale_a: torch.Tensor,
+                            ptr_scale_b: torch.Tensor, ptr_Cs: torch.Tensor, h_problem_sizes: Sequence[tuple],
+                            h_qbits_list: Sequence[QParams]) -> None:
+    """Call the drop-in ``groupgemm_mxmoe`` entry (reference FuncType, registry.cuh:28-39).
+
+    ``ptr_*`` are int64 device tensors holding device pointers (the reference's device arrays).
+    """
+    P = len(h_problem_sizes)
+    dims = (nat.MxmoeDim3 * max(P, 1))(*[nat.MxmoeDim3(int(m), int(n), int(k)) for (m, n, k) in h_problem_sizes])
+    qps = (nat.MxmoeQParams * max(P, 1))(
+        *[nat.MxmoeQParams(q.a_bits, q.w_bits, q.gsize, int(q.sym), (ctypes.c_uint8 * 3)()) for q in h_qbits_list])
+    dev_dims = torch.tensor([[m, n, k] for (m, n, k) in h_problem_sizes], dtype=torch.int32, device=ptr_As.device)
+    nat.check(nat.lib().groupgemm_mxmoe(
+        ptr_As.data_ptr(), ptr_Bs.data_ptr(), ptr_scale_a.data_ptr(), ptr_scale_b.data_ptr(), ptr_Cs.data_ptr(),
+        None, None, None, None, None, ctypes.c_void_p(dev_dims.data_ptr()), dims, None, qps, P))

@@ -1,0 +1,73 @@
+"""Input preparation for quantised GroupGEMM problems (bench / test setup — not the hot path).
+
+Restates, in torch (runs on CPU or on the GPU for the bs=8192 shapes):
+  * ``quant_rtn_sym``: RTN per-row symmetric quantisation in fp16, the reference's
+    ``quant_weight`` kernel (mxmoe/kernels/src/include/quantize.cuh:218-279) and
+    ``quant_minmax`` (mxmoe/quant/quant.py:40-84): scale = fp16(max|x| / qmax) (0 -> 1),
+    q = round_half_even(clamp(fp16(x / scale), -qmax, qmax)).
+  * ``pack_wxax``: the 16-bit word packing of ``pack_wxax`` (quantize.cuh:425-475): element
+    j+x of a word sits at bits (PACK-1-x)*bits (first element in the HIGH bits), two's complement
+    fields, little-endian words.  int8: byte[2j] = q[2j+1], byte[2j+1] = q[2j];
+    int4: byte[2j] = (q[4j+2] << 4) | q[4j+3], byte[2j+1] = (q[4j] << 4) | q[4j+1].
+"""
+from __future__ import annotations
+
+import torch
+
+
+def qmax_of(bits: int) -> int:
+    return (1 << (bits - 1)) - 1
+
+
+def quant_rtn_sym(x: torch.Tensor, bits: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-row (gsize -1) symmetric RTN of an fp16 [rows, K] tensor -> (int8 codes, fp16 scale[rows])."""
+    if x.dtype != torch.float16:
+        raise TypeError("quant_rtn_sym expects fp16 input (the reference quantises in half)")
+    if bits not in (4, 8):
+        raise ValueError("only 4/8-bit WxAx quantisation is supported")
+    qmax = qmax_of(bits)
+    amax = x.abs().amax(dim=-1)
+    scale = amax / qmax  # fp16 / int -> fp16, correctly rounded
+    scale = torch.where(scale == 0, torch.ones_like(scale), scale)
+    q = (x / scale[..., None]).clamp(-qmax, qmax).round()  # round = half to even
+    return q.to(torch.int8), scale
+
+
+def pack_wxax(q: torch.Tensor, bits: int) -> torch.Tensor:
+    """int8 codes [rows, K] -> packed bytes uint8 [rows, K*bits/8] (reference pack_wxax layout)."""
+    rows, K = q.shape
+    if bits == 8:
+        if K % 2:
+            raise ValueError("pack_dim not aligned with pack_num")
+        w = q.reshape(rows, K // 2, 2)
+        out = torch.stack([w[..., 1], w[..., 0]], dim=-1)
+        return out.reshape(rows, K).view(torch.uint8)
+    if bits == 4:
+        if K % 4:
+            raise ValueError("pack_dim not aligned with pack_num")
+        n = (q.to(torch.int16) & 0xF).reshape(rows, K // 4, 4)
+        b0 = (n[..., 2] << 4) | n[..., 3]
+        b1 = (n[..., 0] << 4) | n[..., 1]
+        return torch.stack([b0, b1], dim=-1).reshape(rows, K // 2).to(torch.uint8)
+    raise ValueError("only support [4, 8] bits sym quantization")
+
+
+def unpack_wxax(p: torch.Tensor, bits: int, K: int) -> torch.Tensor:
+    """Inverse of pack_wxax: packed bytes -> int8 codes [rows, K] in logical order."""
+    rows = p.shape[0]
+    if bits == 8:
+        w = p.view(torch.int8).reshape(rows, K // 2, 2)
+        return torch.stack([w[..., 1], w[..., 0]], dim=-1).reshape(rows, K)
+    if bits == 4:
+        b = p.to(torch.int16).reshape(rows, K // 4, 2)
+        b0, b1 = b[..., 0], b[..., 1]
+        nib = torch.stack([(b1 >> 4) & 0xF, b1 & 0xF, (b0 >> 4) & 0xF, b0 & 0xF], dim=-1)
+        nib = torch.where(nib >= 8, nib - 16, nib)
+        return nib.reshape(rows, K).to(torch.int8)
+    raise ValueError("only support [4, 8] bits")
+
+
+def quantize_pack(x: torch.Tensor, bits: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """fp16 [rows, K] -> (packed uint8, fp16 scale, int8 codes)."""
+    q, s = quant_rtn_sym(x, bits)
+    return pack_wxax(q, bits), s, q

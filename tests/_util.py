@@ -1,0 +1,69 @@
+"""Shared helpers for tests: seeded problem construction + oracle expectations."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, Problem, QParams
+from mxmoe_amd.quantize import pack_wxax, quant_rtn_sym
+from oracle import oracle
+
+QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4}
+
+
+class HostProblem:
+    """Host copies of one problem's inputs (numpy) + the device Problem."""
+
+    def __init__(self, M, N, K, q: QParams, seed: int, device: str, ldc: int = 0, C: torch.Tensor | None = None,
+                 c_col0: int = 0):
+        g = torch.Generator().manual_seed(seed)
+        self.M, self.N, self.K, self.q = M, N, K, q
+        a = (torch.rand(M, K, generator=g, dtype=torch.float32) * 2 - 1).to(torch.float16)
+        b = (torch.rand(N, K, generator=g, dtype=torch.float32) * 2 - 1).to(torch.float16)
+        if q.is_quant:
+            bits = q.a_bits
+            qa, sa = quant_rtn_sym(a, bits)
+            qb, sb = quant_rtn_sym(b, bits)
+            self.qa, self.qb = qa.numpy(), qb.numpy()
+            self.A = pack_wxax(qa, bits).numpy()
+            self.B = pack_wxax(qb, bits).numpy()
+            self.sa, self.sb = sa.numpy(), sb.numpy()
+        else:
+            self.A, self.B = a.numpy(), b.numpy()
+            self.sa = self.sb = None
+        self.ldc = ldc or N
+        dev = torch.device(device)
+        if C is None:
+            self.Cbuf = torch.full((max(M, 1), self.ldc), float("nan"), dtype=torch.float16, device=dev)
+            Cview = self.Cbuf
+        else:
+            self.Cbuf = C
+            Cview = C[:, c_col0:]
+        self.c_col0 = c_col0
+        self.problem = Problem(
+            A=torch.from_numpy(self.A).to(dev), B=torch.from_numpy(self.B).to(dev), C=Cview, M=M, N=N, K=K, q=q,
+            scale_a=None if self.sa is None else torch.from_numpy(self.sa).to(dev),
+            scale_b=None if self.sb is None else torch.from_numpy(self.sb).to(dev),
+            ldc=self.ldc if C is None else C.shape[1])
+
+    def expected(self) -> np.ndarray:
+        if self.q.is_quant:
+            return oracle.gg_quant(self.A, self.B, self.sa, self.sb, self.M, self.N, self.K, self.q.a_bits)
+        return oracle.gg_f16(self.A, self.B, self.M, self.N, self.K)
+
+    def result(self) -> np.ndarray:
+        c = self.problem.C
+        return c[: self.M, : self.N].cpu().numpy()
+
+
+def assert_f16_close(out: np.ndarray, ref: np.ndarray, K: int):
+    """fp16 GroupGEMM tolerance: relative 1e-3 (north_star) plus an absolute floor for cancellation,
+    |out-ref| <= 1e-3*|ref| + 1e-3*rms(ref) + 2^-10 * (K * 2^-24 * |a||b| bound ~ 0)."""
+    out = out.astype(np.float64)
+    ref = ref.astype(np.float64)
+    assert np.isfinite(out).all(), "non-finite output"
+    rms = float(np.sqrt(np.mean(ref * ref))) if ref.size else 0.0
+    tol = 1e-3 * np.abs(ref) + 1e-3 * rms + 1e-6
+    bad = np.abs(out - ref) > tol
+    assert not bad.any(), f"{bad.sum()} / {bad.size} fp16 outputs outside tolerance; max err " \
+                          f"{np.max(np.abs(out - ref))}"
