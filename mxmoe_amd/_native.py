@@ -39,7 +39,6 @@ class GGError(RuntimeError):
 class MxmoeQParams(ctypes.Structure):
     """Layout of the reference's mxmoe::QParams (quantize.cuh:14-25): int2 qbits; int gsize; bool sym."""
 
-    _pack_ = 8
     _fields_ = [("a_bits", ctypes.c_int32), ("w_bits", ctypes.c_int32), ("gsize", ctypes.c_int32),
                 ("sym", ctypes.c_uint8), ("pad_", ctypes.c_uint8 * 3)]
 

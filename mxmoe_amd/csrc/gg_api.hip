@@ -138,7 +138,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (lda_b < kbytes || ldb_b < kbytes || (lda_b % 16) || (ldb_b % 16))
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: lda/ldb must be >= K row and a multiple of 8 words", idx);
   if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
-  if (check_ptrs) {
+  if (check_ptrs && p.M > 0 && p.N > 0) {  // empty problems are dropped by the planner
     if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
     if (qt != QT_F16 && (!p.SA || !p.SB)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer", idx);
     if (((uintptr_t)p.A | (uintptr_t)p.B | (uintptr_t)p.C) & 15)

@@ -276,7 +276,11 @@ __device__ __forceinline__ void gg_tile(const GGMeta& mt, const uint8_t* __restr
         for (int j = 0; j < FN; ++j) {
           const int lc = wn * Cfg::WTN + j * 16 + r16;
           const _Float16 s16 = sa * sb[j];  // fp16 product, RN (mm_tile.cuh:490-493)
-          const float v = 0.0f + (float)(acc[i][j][r] >> SHIFT) * (float)s16;
+          // the reference rounds the product to f32 and then to fp16 (double rounding); the
+          // empty asm keeps hipcc from fusing mul + cvt into one v_fma_mix (single rounding)
+          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
+          asm volatile("" : "+v"(prod));
+          const float v = 0.0f + prod;
           Cs[lr * Cfg::C_STRIDE + lc] = (_Float16)v;
         }
       }

@@ -1,0 +1,104 @@
+"""Bench harness — the Python restatement of the reference's C++ harness (src/test.cu, test_utils.h).
+
+Reference behaviour mirrored:
+  * inputs: uniform(-1, 1) fp16 A/B per problem, seeded (test.cu:877-915: default_random_engine(42));
+    quantised problems are RTN-quantised per row and packed (QInput::from_fp16, test.cu:218-413) —
+    unlike the reference bench (test.cu:518-521), the packed ints really are the quantised values
+  * FLOPs = sum 2*M*N*K; TFLOPS = FLOPs / median_ms * 1e3 / 1e12 (test.cu:116, 154)
+  * timing: up to 30 warmups, 50 timed iterations, median (test_utils.h:97-191)
+  * CSV: kernel_name,avg_time,TFLOPS,speedup (test.cu:855-865)
+Inputs are generated on the GPU (torch) so bs=8192 layers build in seconds; this is setup, not the
+hot path.
+"""
+from __future__ import annotations
+
+import csv
+import dataclasses
+import os
+import statistics
+from typing import Optional, Sequence
+
+import torch
+
+from .groupgemm import GroupGemm, Problem, QParams
+from .quantize import pack_wxax, quant_rtn_sym
+from .workload import QShape
+
+
+@dataclasses.dataclass
+class LayerInputs:
+    problems: list[Problem]
+    shapes: list[QShape]
+
+    @property
+    def flops(self) -> int:
+        return sum(s.flops for s in self.shapes)
+
+    def bytes_algorithmic(self) -> int:
+        """Packed A + packed B + fp16 C + fp16 scales."""
+        tot = 0
+        for s in self.shapes:
+            ab = 16 if s.qcfg == "fp16" else s.a_bits
+            wb = 16 if s.qcfg == "fp16" else s.w_bits
+            tot += (s.M * s.K * ab + s.N * s.K * wb) // 8 + 2 * s.M * s.N
+            if s.qcfg != "fp16":
+                tot += 2 * (s.M + s.N)
+        return tot
+
+
+def build_layer_inputs(shapes: Sequence[QShape], device="cuda", seed: int = 42,
+                       out: Optional[torch.Tensor] = None) -> LayerInputs:
+    """Allocate + fill one GroupGEMM call's inputs on `device` (one generator, problem order)."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    probs = []
+    for s in shapes:
+        M, N, K = s.M, s.N, s.K
+        q = QParams(a_bits=s.a_bits, w_bits=s.w_bits, gsize=s.gsize, sym=s.sym)
+        a = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).to(torch.float16)
+        b = (torch.rand(N, K, generator=g, device=dev) * 2 - 1).to(torch.float16)
+        C = torch.empty(max(M, 1), N, dtype=torch.float16, device=dev)
+        if q.is_quant:
+            qa, sa = quant_rtn_sym(a, q.a_bits)
+            qb, sb = quant_rtn_sym(b, q.w_bits)
+            A, B = pack_wxax(qa, q.a_bits), pack_wxax(qb, q.w_bits)
+            del qa, qb
+            probs.append(Problem(A=A, B=B, C=C, M=M, N=N, K=K, q=q, scale_a=sa, scale_b=sb))
+        else:
+            probs.append(Problem(A=a, B=b, C=C, M=M, N=N, K=K, q=q))
+        del a, b
+    return LayerInputs(problems=probs, shapes=list(shapes))
+
+
+def time_launches(fn, warmup: int = 20, iters: int = 50, stream: Optional[torch.cuda.Stream] = None) -> dict:
+    """Per-call device time with events on the launch stream; median / mean / min in ms."""
+    s = stream if stream is not None else torch.cuda.current_stream()
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for a, b in ev:
+        a.record(s)
+        fn()
+        b.record(s)
+    torch.cuda.synchronize()
+    ts = [a.elapsed_time(b) for a, b in ev]
+    return {"median_ms": statistics.median(ts), "mean_ms": sum(ts) / len(ts), "min_ms": min(ts), "iters": iters}
+
+
+def bench_call(inputs: LayerInputs, variant: int = 0, warmup: int = 20, iters: int = 50) -> dict:
+    gg = GroupGemm(inputs.problems, variant=variant)
+    t = time_launches(gg.launch, warmup, iters)
+    t["tflops"] = inputs.flops / (t["median_ms"] * 1e-3) / 1e12
+    t["tiles"] = gg.total_tiles
+    return t
+
+
+def write_csv(path: str, rows: list[dict]) -> None:
+    """CSV in the reference bench schema (test.cu:855-865)."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel_name", "avg_time", "TFLOPS", "speedup"])
+        for r in rows:
+            w.writerow([r["kernel_name"], f"{r['avg_time']:.6f}", f"{r['TFLOPS']:.3f}", f"{r['speedup']:.3f}"])

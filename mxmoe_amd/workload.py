@@ -1,0 +1,216 @@
+"""Workload JSON surface (problem lists per layer) — mirrors mxmoe/kernels/gen_workload.py.
+
+Reference behaviour kept (SeaCatComplexes/MxMoE, gen_workload.py):
+  * MODEL_ID_TO_LAYERS ............................................. :16-21
+  * qstr -> {w_bits, a_bits, gsize, sym} parsing .................... :51-57
+  * per routed expert e: gate_up [int(p_e*T*topk), 2N, K], down [int(p_e*T*topk), K, N] .. :93-96
+  * shared expert appended last: gate_up [T, 2N*S, K], down [T, K, N*S] (S may be a float) .. :99-101
+  * the shared expert's down projection takes the "gate" qcfg (reference behaviour, :101) — kept
+    by default so generated workloads match the reference byte for byte (``shared_down_qcfg``)
+  * output JSON {"num_tokens": T, "layer-L": {"gate_up": [...], "down": [...]}} .... :68-106
+The workload JSON is read like test.cu's parse_json_input (test.cu:652-674): floats -> int.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from pathlib import Path
+from typing import Literal, Optional
+
+import numpy as np
+
+from .qconfig import load_qconfig
+
+WORKLOAD_DIR = Path(__file__).resolve().parent / "workloads"
+
+MODEL_ID_TO_LAYERS = {
+    "qwen2_moe": 24,
+    "qwen2_moe_57b": 28,
+    "ds2": 27,
+    "mixtral": 32,
+}
+
+# MoE geometry per model (moe_tracer.py:42-56; public model configs): hidden K, expert intermediate N,
+# routed experts, top-k, shared experts (as the multiplier S used by gen_workload.py:99-101).
+MODEL_SHAPES = {
+    "qwen2_moe": dict(K=2048, N=1408, E=60, topk=4, S=4.0),
+    "ds2": dict(K=2048, N=1408, E=64, topk=6, S=2),
+    "qwen2_moe_57b": dict(K=3584, N=2560, E=64, topk=8, S=8.0),
+    "mixtral": dict(K=4096, N=14336, E=8, topk=2, S=0),
+}
+
+
+@dataclasses.dataclass
+class QShape:
+    """One problem of a workload (test.cu:63-87)."""
+
+    shape: list
+    w_bits: int = 16
+    a_bits: int = 16
+    gsize: int = -1
+    sym: bool = True
+
+    @property
+    def M(self) -> int:
+        return int(self.shape[0])
+
+    @property
+    def N(self) -> int:
+        return int(self.shape[1])
+
+    @property
+    def K(self) -> int:
+        return int(self.shape[2])
+
+    @property
+    def qcfg(self) -> str:
+        if self.w_bits == 16 and self.a_bits == 16:
+            return "fp16"
+        return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}"
+
+    @property
+    def flops(self) -> int:
+        return 2 * self.M * self.N * self.K
+
+    def to_json(self) -> dict:
+        return {"shape": list(self.shape), "w_bits": self.w_bits, "a_bits": self.a_bits, "gsize": self.gsize,
+                "sym": self.sym}
+
+    @staticmethod
+    def from_json(j: dict) -> "QShape":
+        return QShape(shape=[int(x) for x in j["shape"]], w_bits=int(j["w_bits"]), a_bits=int(j["a_bits"]),
+                      gsize=int(j["gsize"]), sym=bool(j["sym"]))
+
+
+def parse_qstr(qstr: str) -> dict:
+    """gen_workload.py:51-57."""
+    return {
+        "w_bits": int(qstr.split("w")[1].split("a")[0]),
+        "a_bits": int(qstr.split("a")[1].split("_g")[0]),
+        "gsize": int(qstr.split("_g")[1].split("_")[0]),
+        "sym": "asym" not in qstr,
+    }
+
+
+FP16_QCFG = {"w_bits": 16, "a_bits": 16, "gsize": -1, "sym": True}
+
+
+def freq_to_prob(freq: list) -> list:
+    total = sum(freq)
+    return [f / total for f in freq]
+
+
+def generate_workload_from_trace(trace: dict, num_total_tokens: int, layer_id: int = -1,
+                                 qconfig: Optional[dict] = None, qstr: Optional[str] = None,
+                                 shared_down_qcfg: Literal["gate", "down"] = "gate") -> dict:
+    """Problem lists for every (or one) layer of a gate trace (gen_workload.py:38-110)."""
+    if qconfig is not None and qstr is not None:
+        raise ValueError("qconfig and qstr are exclusive")
+    if qconfig is not None:
+        qconfig = {k: v for k, v in qconfig.items() if k != "LT"}
+        uni = None
+    else:
+        uni = parse_qstr(qstr) if qstr is not None else dict(FP16_QCFG)
+
+    topk = trace["topk"]
+    N, K = trace["NK"]
+    S = trace["num_shared_experts"]
+    result: dict = {"num_tokens": num_total_tokens}
+    for key, value in trace.items():
+        if not key.startswith("layer-"):
+            continue
+        layer_idx = key.split("-")[1]
+        if layer_id != -1 and layer_idx != str(layer_id):
+            continue
+
+        def lin(exp_idx: str, linear: str) -> dict:
+            if uni is not None:
+                return dict(uni)
+            c = qconfig[layer_idx]["experts"][exp_idx][linear]
+            return {"w_bits": c["w_bits"], "a_bits": c["a_bits"], "gsize": c["w_gsize"], "sym": c["w_sym"]}
+
+        prob = freq_to_prob(value["access_freq"])
+        E = len(prob)
+        shapes: dict = {"gate_up": [], "down": []}
+        for e, p in enumerate(prob):
+            m = int(p * num_total_tokens * topk)
+            shapes["gate_up"].append({"shape": [m, N * 2, K], **lin(str(e), "gate")})
+            shapes["down"].append({"shape": [m, K, N], **lin(str(e), "down")})
+        if S != 0:
+            shapes["gate_up"].append({"shape": [int(num_total_tokens), N * 2 * S, K], **lin(str(E), "gate")})
+            shapes["down"].append({"shape": [int(num_total_tokens), K, N * S], **lin(str(E), shared_down_qcfg)})
+        result[f"layer-{layer_idx}"] = shapes
+    return result
+
+
+def save_workload(wl: dict, path: str) -> None:
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(wl, f, indent=2)
+
+
+def load_workload(path_or_dict) -> dict[str, dict[str, list[QShape]]]:
+    """Parse a workload JSON (test.cu:652-674): {layer: {gate_up|down: [QShape]}}; num_tokens skipped."""
+    if isinstance(path_or_dict, dict):
+        d = path_or_dict
+    else:
+        with open(path_or_dict) as f:
+            d = json.load(f)
+    out = {}
+    for k, v in d.items():
+        if k == "num_tokens":
+            continue
+        out[k] = {gg: [QShape.from_json(p) for p in lst] for gg, lst in v.items()}
+    return out
+
+
+# ---------------------------------------------------------------- synthetic workloads (bench)
+
+def qwen2_hist() -> dict:
+    with open(WORKLOAD_DIR / "qwen2_moe_hist_bs8192.json") as f:
+        return json.load(f)
+
+
+def qwen2_layer11_trace(bs_ref: int = 8192) -> dict:
+    """A gate trace whose layer-11 access frequencies are the committed bs=8192 histogram (§8d)."""
+    h = qwen2_hist()
+    return {"topk": h["topk"], "NK": [h["moe_intermediate"], h["hidden"]], "num_shared_experts": h["num_shared_experts"],
+            "layer-11": {"access_freq": h["M"]}}
+
+
+def qwen2_layer11_workload(bs: int = 8192, qconfig: Optional[dict] = None, qstr: Optional[str] = None) -> dict:
+    """qwen2_moe 'layer-11' problems. At bs=8192 the routed M_e are exactly the committed histogram."""
+    h = qwen2_hist()
+    if bs == h["num_tokens"]:
+        wl = generate_workload_from_trace(qwen2_layer11_trace(), bs, 11, qconfig=qconfig, qstr=qstr)
+        for gg in ("gate_up", "down"):  # int(p*T*topk) truncation differs by <=1 row: pin the committed M_e
+            for p, m in zip(wl["layer-11"][gg][:-1], h["M"]):
+                p["shape"][0] = m
+        return wl
+    return generate_workload_from_trace(qwen2_layer11_trace(), bs, 11, qconfig=qconfig, qstr=qstr)
+
+
+def ds2_trace(bs: int = 8192, seed: int = 0) -> dict:
+    """DeepSeek-V2-Lite routing: M_e ~ multinomial(bs*6, dirichlet(20*1_64))."""
+    s = MODEL_SHAPES["ds2"]
+    rng = np.random.default_rng(seed)
+    p = rng.dirichlet(20.0 * np.ones(s["E"]))
+    m = rng.multinomial(bs * s["topk"], p)
+    return {"topk": s["topk"], "NK": [s["N"], s["K"]], "num_shared_experts": s["S"],
+            "layer-1": {"access_freq": [int(x) for x in m]}}
+
+
+def ds2_workload(bs: int = 8192, qconfig: Optional[dict] = None, qstr: Optional[str] = None, seed: int = 0) -> dict:
+    return generate_workload_from_trace(ds2_trace(bs, seed), bs, 1, qconfig=qconfig, qstr=qstr)
+
+
+def mixed_qconfig_lp1() -> dict:
+    """The committed mixed w4a4+w8a8 (wbits 5.0) qconfig solved from the reference's bits_model-1.lp."""
+    return load_qconfig(WORKLOAD_DIR / "qconfig_qwen2_moe_w4a4+w8a8_wbits5.0_lp1.json")
+
+
+def layer_problems(wl: dict, layer: Optional[str] = None) -> dict[str, list[QShape]]:
+    parsed = load_workload(wl)
+    key = layer or next(iter(parsed))
+    return parsed[key]

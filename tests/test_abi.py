@@ -1,0 +1,102 @@
+"""C-ABI tests that need no GPU: the library loads, exports exactly what include/mxmoe_gg.h declares,
+struct layouts match the reference's, and host-side validation rejects bad problems with status codes."""
+from __future__ import annotations
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from mxmoe_amd import _native as nat
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "mxmoe_gg.h"
+
+
+def header_functions() -> set:
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(\w+)\s*\(", txt, flags=re.M)) - {"defined"}
+
+
+def test_header_lists_all_python_bound_symbols():
+    assert header_functions() == set(nat.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_header_symbol():
+    lib = nat.lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(nat.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert header_functions() <= exported
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(nat.MxmoeQParams) == 16  # QParams: 16-B stride, as int2+int+bool (8-B aligned)
+    assert ctypes.sizeof(nat.MxmoeDim3) == 12
+    assert ctypes.sizeof(nat.GGProblemC) == 5 * 8 + 8 * 4 + 3 * 8
+
+
+def test_abi_version_and_variants():
+    assert nat.lib().mxmoe_gg_abi_version() == 1
+    vs = nat.list_variants()
+    assert len(vs) == nat.variant_count() >= 1
+    assert "w8a8_g-1_sym=TileConfig(" in vs[0]
+    t = nat.variant_tile(0, 8, 8)
+    assert t["BM"] > 0 and t["BN"] > 0 and t["threads"] % 64 == 0
+
+
+def test_workspace_size_monotone():
+    assert nat.workspace_size(1) <= nat.workspace_size(61) <= nat.workspace_size(1000)
+
+
+def _plan(problems, ws_bytes=1 << 20):
+    arr = (nat.GGProblemC * len(problems))(*problems)
+    info = nat.GGPlanInfo()
+    st = nat.lib().mxmoe_gg_plan(arr, len(problems), 0, None, ws_bytes, None, ctypes.byref(info))
+    return st, nat.lib().mxmoe_gg_last_error().decode()
+
+
+def _prob(**kw):
+    d = dict(A=16, B=16, scale_a=16, scale_b=16, C=16, M=64, N=128, K=256, a_bits=8, w_bits=8, gsize=-1, sym=1)
+    d.update(kw)
+    return nat.GGProblemC(**d)
+
+
+@pytest.mark.parametrize("kw,status,msg", [
+    (dict(a_bits=4, w_bits=16, sym=0), nat.MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported"),
+    (dict(gsize=128), nat.MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported"),
+    (dict(K=24), nat.MXMOE_GG_ERR_INVALID, "multiple of 16"),
+    (dict(N=100), nat.MXMOE_GG_ERR_INVALID, "multiple of 8"),
+    (dict(M=-1), nat.MXMOE_GG_ERR_INVALID, "negative"),
+    (dict(A=0), nat.MXMOE_GG_ERR_INVALID, "NULL"),
+    (dict(scale_b=0), nat.MXMOE_GG_ERR_INVALID, "NULL scale"),
+    (dict(C=8), nat.MXMOE_GG_ERR_INVALID, "aligned"),
+    (dict(ldc=100), nat.MXMOE_GG_ERR_INVALID, "ldc"),
+    (dict(K=262144), nat.MXMOE_GG_ERR_INVALID, "exact int32"),
+])
+def test_plan_validation(kw, status, msg):
+    st, err = _plan([_prob(), _prob(**kw)])
+    assert st == status
+    assert msg in err and "problem 1" in err
+
+
+def test_plan_needs_workspace():
+    st, err = _plan([_prob()], ws_bytes=0)
+    assert st == nat.MXMOE_GG_ERR_WORKSPACE and "workspace" in err
+
+
+def test_fp16_problem_needs_no_scales():
+    st, err = _plan([_prob(a_bits=16, w_bits=16, scale_a=0, scale_b=0)], ws_bytes=0)
+    assert st == nat.MXMOE_GG_ERR_WORKSPACE  # passed validation, stopped at the workspace check
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(nat, "_lib", None)
+    monkeypatch.setenv("MXMOE_GG_LIB", str(tmp_path / "nope.so"))
+    with pytest.raises(nat.NativeLibraryError):
+        nat.lib()
+    monkeypatch.setattr(nat, "_lib", None)
