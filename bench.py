@@ -1,0 +1,275 @@
+"""bench.py — GroupGEMM TFLOP/s + %roofline, qwen2_moe layer-11 (bs=8192), MI355X.
+
+One "step" = one pass of the hot path over one batch: the layer's two fused GroupGEMM calls
+(gate_up: 61 problems, down: 61 problems), inputs resident in HBM, tile tables planned once.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config fp16|w8a8|w4a4|mixed] [--variant V]
+  (N > 1: launched by torch.distributed.run, one rank per GPU)
+
+Multi-GPU (weak scaling, expert parallel): with N ranks the global batch is N x 8192 tokens and the
+routed experts are sharded by index across ranks (LPT on expert cost); rank r runs its experts with
+M = N * M_e rows (the tokens routed to them from the whole global batch) plus the replicated shared
+expert on its local 8192 tokens. Per-rank work stays ~ one layer; there is no collective inside the
+GroupGEMM (token dispatch/combine is MoE-layer plumbing outside this path).
+value = FLOPs of all ranks / max-over-ranks time of K steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+PEAK_TFLOPS = {"fp16": 2500.0, "int8": 5000.0}  # dense MFMA peaks, MI355X_MICROARCH.md (spec)
+HBM_GBS = 8000.0
+
+CONFIGS = {
+    "fp16": dict(kw={}, peak="fp16", dtype="fp16", name="qwen2_moe layer-11 fp16 GroupGEMM bs=8192, 60 experts"),
+    "w8a8": dict(kw=dict(qstr="w8a8_g-1_sym"), peak="int8", dtype="int8",
+                 name="qwen2_moe layer-11 w8a8_g-1_sym GroupGEMM bs=8192 (int8 MFMA)"),
+    "w4a4": dict(kw=dict(qstr="w4a4_g-1_sym"), peak="int8", dtype="int4",
+                 name="qwen2_moe layer-11 w4a4_g-1_sym GroupGEMM bs=8192 (int8 MFMA)"),
+    "mixed": dict(kw="mixed", peak="int8", dtype="int4+int8",
+                  name="qwen2_moe layer-11 mixed w4a4+w8a8 (wbits=5.0, LP-1 qconfig) bs=8192"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def layer_shapes(cfg: str, world: int, rank: int, bs: int = 8192):
+    """Per-rank problem lists {gate_up, down} (expert-parallel weak scaling, see module doc)."""
+    from mxmoe_amd.workload import QShape, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+
+    kw = CONFIGS[cfg]["kw"]
+    if kw == "mixed":
+        kw = dict(qconfig=mixed_qconfig_lp1())
+    wl = load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
+    if world == 1:
+        return wl
+    routed = list(range(len(wl["gate_up"]) - 1))
+    # LPT: heaviest expert (gate_up+down FLOPs at global M) to the least-loaded rank
+    cost = {e: wl["gate_up"][e].flops + wl["down"][e].flops for e in routed}
+    load = [0] * world
+    owner = {}
+    for e in sorted(routed, key=lambda e: -cost[e]):
+        r = min(range(world), key=lambda r: load[r])
+        owner[e] = r
+        load[r] += cost[e]
+    out = {}
+    for gg in ("gate_up", "down"):
+        lst = []
+        for e in routed:
+            if owner[e] == rank:
+                s = wl[gg][e]
+                lst.append(QShape([s.M * world, s.N, s.K], s.w_bits, s.a_bits, s.gsize, s.sym))
+        lst.append(wl[gg][-1])  # shared expert, local tokens
+        out[gg] = lst
+    return out
+
+
+def cpu_baseline(cfg: str, shapes, budget_s: float = 12.0) -> dict:
+    """The CPU oracle (port of the reference arithmetic) timed on this host's cores, bounded sample."""
+    import numpy as np
+
+    from oracle import oracle
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    rng = np.random.default_rng(0)
+    done_flops, t_used, names = 0, 0.0, []
+    probs = [(gg, s) for gg in ("gate_up", "down") for s in shapes[gg][:-1]]
+    for gg, s in probs[::7]:
+        M, N, K = s.M, s.N, s.K
+        if s.qcfg == "fp16":
+            A = (rng.random((M, K), np.float32) * 2 - 1).astype(np.float16)
+            B = (rng.random((N, K), np.float32) * 2 - 1).astype(np.float16)
+            t0 = time.perf_counter()
+            oracle.gg_f16(A, B, M, N, K, threads)
+        else:
+            bits = s.a_bits
+            A = rng.integers(0, 256, (M, K * bits // 8), dtype=np.uint8)
+            B = rng.integers(0, 256, (N, K * bits // 8), dtype=np.uint8)
+            sa = (rng.random(M, np.float32) * 0.01).astype(np.float16)
+            sb = (rng.random(N, np.float32) * 0.01).astype(np.float16)
+            t0 = time.perf_counter()
+            oracle.gg_quant(A, B, sa, sb, M, N, K, bits, threads)
+        t_used += time.perf_counter() - t0
+        done_flops += 2 * M * N * K
+        names.append(f"{gg}[{M}x{N}x{K} {s.qcfg}]")
+        if t_used > budget_s:
+            break
+    return {"value": round(done_flops / t_used / 1e12, 6), "unit": "TFLOP/s", "cores": threads, "kind": "port",
+            "sample": f"{len(names)} routed-expert problems of the same layer ({', '.join(names)}), "
+                      f"{done_flops / 1e9:.1f} GFLOP in {t_used:.1f} s; oracle/gg_oracle.c (OpenMP, "
+                      f"{platform.processor() or platform.machine()})"}
+
+
+def load_pmc_traffic(cfg: str):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(cfg)
+    except Exception:  # pragma: no cover
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="fp16", choices=list(CONFIGS))
+    ap.add_argument("--variant", type=int, default=-1, help="-1 = default variant for the config")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extras", default="w8a8,mixed", help="other configs measured as extra fields (N=1)")
+    ap.add_argument("--median-iters", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from mxmoe_amd import _native as nat
+    from mxmoe_amd.groupgemm import GroupGemm
+    from mxmoe_amd.harness import build_layer_inputs, time_launches
+
+    def run_config(cfg: str, steps: int, warmup: int, timed_region: bool):
+        variant = args.variant if args.variant >= 0 else default_variant(cfg)
+        shapes = layer_shapes(cfg, world, rank)
+        inp = {gg: build_layer_inputs(shapes[gg], device=dev, seed=42 + 1000 * rank + (gg == "down"))
+               for gg in ("gate_up", "down")}
+        ggs = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
+        flops = {gg: inp[gg].flops for gg in inp}
+        stream = torch.cuda.current_stream(dev)
+
+        def step():
+            ggs["gate_up"].launch(stream)
+            ggs["down"].launch(stream)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        res = {}
+        if timed_region:
+            if world > 1:
+                torch.distributed.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            if world > 1:
+                torch.distributed.barrier()
+                t = torch.tensor([dt], device=dev, dtype=torch.float64)
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+                dt = float(t.item())
+                f = torch.tensor([float(flops["gate_up"] + flops["down"])], device=dev, dtype=torch.float64)
+                torch.distributed.all_reduce(f)
+                total_flops = float(f.item())
+            else:
+                total_flops = float(flops["gate_up"] + flops["down"])
+            res["dt"] = dt
+            res["total_flops"] = total_flops
+        # per-launch device time (HIP events on the launch stream) — the roofline's denominator
+        per = {gg: time_launches(lambda g=gg: ggs[g].launch(stream), warmup=3, iters=args.median_iters, stream=stream)
+               for gg in ggs}
+        res.update(per=per, flops=flops, variant=variant, tiles={gg: ggs[gg].total_tiles for gg in ggs},
+                   bytes={gg: inp[gg].bytes_algorithmic() for gg in inp}, shapes=shapes)
+        del ggs, inp
+        torch.cuda.empty_cache()
+        return res
+
+    cfg = args.config
+    main_res = run_config(cfg, args.steps, args.warmup, True)
+    peak = PEAK_TFLOPS[CONFIGS[cfg]["peak"]]
+    per = main_res["per"]
+    f_gu, f_dn = main_res["flops"]["gate_up"], main_res["flops"]["down"]
+    t_gu, t_dn = per["gate_up"]["mean_ms"], per["down"]["mean_ms"]
+    achieved = (f_gu + f_dn) / ((t_gu + t_dn) * 1e-3) / 1e12
+    value = main_res["total_flops"] / main_res["dt"] / 1e12
+    pmc = load_pmc_traffic(cfg)
+
+    extras = {}
+    if rank == 0:
+        for gg in ("gate_up", "down"):
+            b = main_res["bytes"][gg]
+            f = main_res["flops"][gg]
+            extras[gg] = {"gflop": round(f / 1e9, 3), "median_ms": round(per[gg]["median_ms"], 4),
+                          "tflops_median": round(f / (per[gg]["median_ms"] * 1e-3) / 1e12, 2),
+                          "tiles": main_res["tiles"][gg], "algorithmic_MB": round(b / 1e6, 1),
+                          "AI_flop_per_B": round(f / b, 1),
+                          "roof_tflops": round(min(peak, f / b * HBM_GBS / 1e3), 1)}
+    if world == 1 and args.extras:
+        for x in [e for e in args.extras.split(",") if e and e != cfg]:
+            r = run_config(x, 0, 3, False)
+            pk = PEAK_TFLOPS[CONFIGS[x]["peak"]]
+            tt = r["per"]["gate_up"]["median_ms"] + r["per"]["down"]["median_ms"]
+            ff = r["flops"]["gate_up"] + r["flops"]["down"]
+            extras[x] = {"tflops": round(ff / (tt * 1e-3) / 1e12, 2),
+                         "gate_up_tflops": round(r["flops"]["gate_up"] / (r["per"]["gate_up"]["median_ms"] * 1e-3) / 1e12, 2),
+                         "down_tflops": round(r["flops"]["down"] / (r["per"]["down"]["median_ms"] * 1e-3) / 1e12, 2),
+                         "roofline_frac": round(ff / (tt * 1e-3) / 1e12 / pk, 4), "peak_tflops": pk,
+                         "variant": r["variant"]}
+
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, main_res["shapes"])
+
+    if rank == 0:
+        out = {
+            "metric": "GroupGEMM TFLOP/s + %roofline, qwen2_moe layer-11 bs=8192 at 1/8 GPU",
+            "value": round(value, 3),
+            "unit": "TFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(main_res["dt"] / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": CONFIGS[cfg]["dtype"],
+            "data": "synthetic: uniform(-1,1) fp16 inputs (seeded) -> RTN per-row quantised + pack_wxax for "
+                    "quantised problems; routed M_e = reference's committed bs=8192 histogram",
+            "config": {"workload": CONFIGS[cfg]["name"] + (f", expert-parallel over {world} GPUs" if world > 1 else ""),
+                       "model": "qwen2_moe (Qwen1.5-MoE-A2.7B) MoE GroupGEMMs", "global_batch": 8192 * world,
+                       "seq_len": None, "parallelism": f"ep{world}" if world > 1 else "single",
+                       "problems_per_call": len(main_res["shapes"]["gate_up"]), "variant": main_res["variant"],
+                       "variant_name": nat.list_variants()[main_res["variant"]].split()[1]},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4),
+                         "traffic": pmc.get("hbm_bytes_per_step") if isinstance(pmc, dict) else None,
+                         "kernel": "mxmoe::gg_fused_kernel (gate_up + down launches)",
+                         "launch_ms": {"gate_up": round(t_gu, 4), "down": round(t_dn, 4)}},
+            "cpu_baseline": cpu,
+            "extras": extras,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def default_variant(cfg: str) -> int:
+    return 0
+
+
+if __name__ == "__main__":
+    main()
