@@ -105,11 +105,13 @@ int mxmoe_gg_list_variants(char* buf, size_t n);
 int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int32_t* bn, int32_t* bk_bytes,
                           int32_t* threads);
 
-/* Device workspace bytes needed for P problems. */
-int mxmoe_gg_workspace_size(int problem_count, size_t* bytes);
+/* Device workspace bytes the plan of these problems needs with this variant
+ * (plan table + pointer arrays + tile table). Validates the problems like mxmoe_gg_plan. */
+int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count, int variant, size_t* bytes);
 
-/* Validate problems, build the tile table and upload it (hipMemcpyAsync on `stream`) into
- * the workspace. Host problem array may be freed after return. */
+/* Validate problems, build the tile table and upload it into the workspace (hipMemcpyAsync on
+ * `stream`, then a stream synchronisation: planning is done once, outside the hot loop).
+ * The host problem array may be freed after return. */
 int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int variant, void* workspace,
                   size_t workspace_bytes, void* stream, mxmoe_gg_plan_info* info);
 

@@ -89,7 +89,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_variant_tile.restype = c.c_int
     lib.mxmoe_gg_variant_tile.argtypes = [c.c_int, c.c_int, c.c_int] + [c.POINTER(c.c_int32)] * 4
     lib.mxmoe_gg_workspace_size.restype = c.c_int
-    lib.mxmoe_gg_workspace_size.argtypes = [c.c_int, c.POINTER(c.c_size_t)]
+    lib.mxmoe_gg_workspace_size.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.POINTER(c.c_size_t)]
     lib.mxmoe_gg_plan.restype = c.c_int
     lib.mxmoe_gg_plan.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
                                   c.POINTER(GGPlanInfo)]
@@ -143,7 +143,8 @@ def variant_tile(variant: int, a_bits: int, w_bits: int) -> dict:
     return {"BM": v[0].value, "BN": v[1].value, "BK_bytes": v[2].value, "threads": v[3].value}
 
 
-def workspace_size(problem_count: int) -> int:
+def workspace_size(problems, problem_count: int, variant: int) -> int:
+    """Workspace bytes for a ctypes array of GGProblemC (plan table + pointers + tile table)."""
     n = ctypes.c_size_t()
-    check(lib().mxmoe_gg_workspace_size(problem_count, ctypes.byref(n)))
+    check(lib().mxmoe_gg_workspace_size(problems, problem_count, variant, ctypes.byref(n)))
     return n.value

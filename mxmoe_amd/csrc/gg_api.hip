@@ -3,10 +3,13 @@
 // Reference behaviour replaced (SeaCatComplexes/MxMoE):
 //   host API groupgemm_hz_fused_<i> ........ kernel_sketch.py:82-145 (prefix sum on host,
 //                                             cudaMalloc/Memcpy/Free per call, grid = #SMs)
+//   tile -> (problem, m, n) by prefix scan .. tile_scheduler.cuh:25-50
 //   registry FuncType / kernel selection ... registry.cuh:28-107, compose_kernel.py:482-529
 //   qtype dispatch + "quant type not supported" ... compose_kernel.py:47-57, 421-479
-// Here: the planner writes a 64-B-per-problem table into a caller-owned workspace once, the
-// launch is allocation- and sync-free (hipGraph capturable), errors are status codes.
+// Here: the planner builds an explicit tile table once into a caller-owned workspace — tiles of
+// the longest problems first (LPT), grouped into chunks of neighbouring tiles that run together on
+// one XCD (shared A rows / B columns hit that XCD's L2) — and the launch is allocation- and
+// sync-free (hipGraph capturable). Errors are status codes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,7 +29,7 @@ namespace {
 thread_local std::string g_last_error;
 
 int fail(int code, const char* fmt, ...) {
-  char buf[512];
+  char buf[768];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
@@ -45,29 +48,57 @@ struct TileGeom {
   int bm, bn, bkb, threads;
 };
 
+enum class Kind { V0, V2 };
+
 struct Variant {
   const char* name;
-  TileGeom geom[QT_COUNT];  // indexed by QType
+  Kind kind;
+  TileGeom geom[QT_COUNT];  // indexed by QType (main tile)
   int threads;
   int lds_bytes;
+  int chunk;           // tiles per XCD chunk (workgroups that run together on one XCD)
+  int k_stage_bytes;   // K bytes per row must be a multiple of this (0 = any multiple of 16)
+  int tail_bm;         // v2: height of the tail-tile class (0 = none)
   void (*launch)(const GGArgs&, int grid, hipStream_t);
 };
 
 template <class C16, class C8, class C4>
-void launch_fused(const GGArgs& a, int grid, hipStream_t s) {
+void launch_v0(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((gg_fused_kernel<C16, C8, C4>), dim3(grid), dim3(C16::kThreads), 0, s, a);
 }
 
+void launch_v2(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(gg_v2_kernel, dim3(grid), dim3(512), 0, s, a);
+}
+
 template <class C16, class C8, class C4>
-Variant make_variant(const char* name) {
+Variant make_v0(const char* name) {
   Variant v;
   v.name = name;
+  v.kind = Kind::V0;
   v.geom[QT_F16] = {C16::BM, C16::BN, C16::BKB, C16::kThreads};
   v.geom[QT_I8] = {C8::BM, C8::BN, C8::BKB, C8::kThreads};
   v.geom[QT_I4] = {C4::BM, C4::BN, C4::BKB, C4::kThreads};
   v.threads = C16::kThreads;
   v.lds_bytes = FusedCfg<C16, C8, C4>::LDS_BYTES;
-  v.launch = &launch_fused<C16, C8, C4>;
+  v.chunk = FusedCfg<C16, C8, C4>::LDS_BYTES <= 80 * 1024 ? 64 : 32;  // workgroups per XCD at once
+  v.k_stage_bytes = 0;
+  v.tail_bm = 0;
+  v.launch = &launch_v0<C16, C8, C4>;
+  return v;
+}
+
+Variant make_v2(const char* name) {
+  Variant v;
+  v.name = name;
+  v.kind = Kind::V2;
+  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 128, 512};
+  v.threads = 512;
+  v.lds_bytes = V2Cfg<256>::LDS_BYTES;
+  v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
+  v.k_stage_bytes = 128;
+  v.tail_bm = 128;
+  v.launch = &launch_v2;
   return v;
 }
 
@@ -77,9 +108,10 @@ typedef TileCfg<128, 256, 2, 2, 1> T128x256;
 
 const std::vector<Variant>& variants() {
   static const std::vector<Variant> v = {
-      make_variant<T128x128, T128x128, T128x128>("fused_128x128_w4"),
-      make_variant<T256x128, T256x128, T256x128>("fused_256x128_w4"),
-      make_variant<T128x256, T128x256, T128x256>("fused_128x256_w4"),
+      make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
+      make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
+      make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
+      make_v2("v2_256x256_w8_dma"),
   };
   return v;
 }
@@ -105,11 +137,6 @@ int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Workspace: [GGMeta x P][ptr_A x P][ptr_B x P][ptr_SA x P][ptr_SB x P][ptr_C x P], 256-B aligned.
-size_t ws_meta_bytes(int P) { return align_up((size_t)P * sizeof(GGMeta), 256); }
-size_t ws_ptr_bytes(int P) { return align_up((size_t)P * sizeof(void*), 256); }
-size_t ws_total_bytes(int P) { return ws_meta_bytes(P) + 5 * ws_ptr_bytes(P); }
-
 struct HostProblem {
   const void *A, *B, *SA, *SB;
   void* C;
@@ -117,7 +144,20 @@ struct HostProblem {
   int64_t lda, ldb, ldc;  // 16-bit words, 0 = dense
 };
 
-// Validate one problem and fill its table row (tile_begin filled by the caller).
+// Workspace: [GGMeta x P][ptr_A x P][ptr_B x P][ptr_SA x P][ptr_SB x P][ptr_C x P][TileDesc x grid]
+struct WsLayout {
+  size_t meta, ptr, tiles, total;
+};
+WsLayout ws_layout(int P, int grid) {
+  WsLayout l;
+  l.meta = align_up((size_t)std::max(P, 1) * sizeof(GGMeta), 256);
+  l.ptr = align_up((size_t)std::max(P, 1) * sizeof(void*), 256);
+  l.tiles = align_up((size_t)std::max(grid, 1) * sizeof(TileDesc), 256);
+  l.total = l.meta + 5 * l.ptr + l.tiles;
+  return l;
+}
+
+// Validate one problem and fill its table row.
 int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs, GGMeta* m) {
   if (p.M < 0 || p.N < 0 || p.K < 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: negative shape", idx);
   int qt = 0;
@@ -128,6 +168,9 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (kbits % 128 != 0)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d must be a multiple of %d for %d-bit data (16-B rows)", idx,
                 p.K, (int)(128 / abits), abits);
+  if (v.k_stage_bytes && (kbits / 8) % v.k_stage_bytes != 0)
+    return fail(MXMOE_GG_ERR_INVALID, "problem %d: variant %s needs K*bits/8 to be a multiple of %d bytes (K=%d)",
+                idx, v.name, v.k_stage_bytes, p.K);
   if (qt != QT_F16 && p.K > 131072)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d exceeds the exact int32 accumulation bound 131072", idx, p.K);
   if (p.N % 8 != 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: N=%d must be a multiple of 8", idx, p.N);
@@ -146,13 +189,12 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
     if (qt != QT_F16 && (((uintptr_t)p.SA | (uintptr_t)p.SB) & 1))
       return fail(MXMOE_GG_ERR_INVALID, "problem %d: scales must be 2-byte aligned", idx);
   }
-  const TileGeom& g = v.geom[qt];
   memset(m, 0, sizeof(*m));
   m->M = p.M;
   m->N = p.N;
   m->K = p.K;
   m->qtype = qt;
-  m->tiles_n = (p.N + g.bn - 1) / g.bn;
+  m->tiles_n = (p.N + v.geom[qt].bn - 1) / v.geom[qt].bn;
   m->kbytes = (int32_t)kbytes;
   m->lda_b = lda_b;
   m->ldb_b = ldb_b;
@@ -160,42 +202,79 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   return MXMOE_GG_OK;
 }
 
-// Plan problems into host buffers. Order: problems with more K bytes per tile (= longer tiles)
-// first, so the longest workgroups are dispatched first and the tail is short (LPT-style).
-int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptrs, std::vector<GGMeta>& meta,
-              std::vector<int>& order, int* total_tiles) {
+struct Plan {
+  std::vector<GGMeta> meta;     // table rows (planned problems only)
+  std::vector<int> order;       // table row -> caller's problem index
+  std::vector<TileDesc> tiles;  // indexed by blockIdx
+  int total_tiles = 0;
+};
+
+// Tile generation + scheduling.
+//  1. per problem: m-tiles of the variant's height (v2: 256-row tiles while > tail_bm rows remain,
+//     then one tail_bm tile), n-tiles of width bn; tiles enumerated in 4-m-tile bands, n-major
+//     inside a band, so 32 consecutive tiles form a ~4 x 8 block sharing A rows and B columns;
+//  2. problems by descending per-tile cost (K bytes x tile area x MFMA passes), longest first;
+//  3. the sequence is cut into chunks of `chunk` tiles; chunk c runs on XCD c % 8 in round c / 8:
+//     blockIdx = 8 * (chunk * round + position) + c % 8 (blocks b and b + 8 share an XCD under the
+//     round-robin dispatch; placement affects speed only, never results).
+int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptrs, Plan* plan) {
   const Variant& v = variants()[variant];
   const int P = (int)probs.size();
   std::vector<GGMeta> all(P);
-  std::vector<int64_t> tiles(P, 0);
   for (int i = 0; i < P; ++i) {
     int st = build_meta(probs[i], i, v, check_ptrs, &all[i]);
     if (st) return st;
-    const TileGeom& g = v.geom[all[i].qtype];
-    if (probs[i].M > 0 && probs[i].N > 0) tiles[i] = (int64_t)((probs[i].M + g.bm - 1) / g.bm) * all[i].tiles_n;
   }
-  order.clear();
+  std::vector<int> order;
   for (int i = 0; i < P; ++i)
-    if (tiles[i] > 0) order.push_back(i);
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-    // per-tile cost ~ tile area * K bytes (MFMA work per byte is equal for int8/int4 and half for fp16)
-    auto cost = [&](int i) {
-      const TileGeom& g = v.geom[all[i].qtype];
-      const double w = all[i].qtype == QT_F16 ? 2.0 : 1.0;
-      return w * (double)g.bm * g.bn * (all[i].qtype == QT_I4 ? 2.0 * all[i].kbytes : (double)all[i].kbytes);
-    };
-    return cost(a) > cost(b);
-  });
-  int64_t acc = 0;
-  meta.clear();
-  for (int i : order) {
-    GGMeta m = all[i];
-    m.tile_begin = (int32_t)acc;
-    acc += tiles[i];
-    meta.push_back(m);
+    if (probs[i].M > 0 && probs[i].N > 0) order.push_back(i);
+  auto tile_cost = [&](int i) {
+    const GGMeta& m = all[i];
+    const double passes = m.qtype == QT_I4 ? 2.0 : 1.0;  // int4: 2 MFMA passes per staged byte
+    return passes * (double)m.kbytes * v.geom[m.qtype].bm * v.geom[m.qtype].bn;
+  };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost(a) > tile_cost(b); });
+
+  plan->meta.clear();
+  plan->order = order;
+  std::vector<TileDesc> seq;
+  for (int row = 0; row < (int)order.size(); ++row) {
+    GGMeta m = all[order[row]];
+    const TileGeom& g = v.geom[m.qtype];
+    std::vector<std::pair<int, int>> mt;  // (m0, cls)
+    for (int m0 = 0; m0 < m.M;) {
+      const int rem = m.M - m0;
+      if (v.kind == Kind::V2 && v.tail_bm && rem <= v.tail_bm) {
+        mt.push_back({m0, 1});
+        m0 += v.tail_bm;
+      } else {
+        mt.push_back({m0, 0});
+        m0 += g.bm;
+      }
+    }
+    m.tile_begin = (int32_t)seq.size();
+    const int nt = m.tiles_n;
+    for (size_t mb = 0; mb < mt.size(); mb += 4)
+      for (int n = 0; n < nt; ++n)
+        for (size_t mi = mb; mi < std::min(mt.size(), mb + 4); ++mi)
+          seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second});
+    plan->meta.push_back(m);
   }
-  if (acc > INT32_MAX / 2) return fail(MXMOE_GG_ERR_INVALID, "too many tiles (%lld)", (long long)acc);
-  *total_tiles = (int)acc;
+  const int T = (int)seq.size();
+  if (T > (1 << 28)) return fail(MXMOE_GG_ERR_INVALID, "too many tiles (%d)", T);
+  const int chunk = v.chunk;
+  const int nchunks = (T + chunk - 1) / chunk;
+  const int rounds = (nchunks + 7) / 8;
+  int grid = 0;
+  plan->tiles.assign((size_t)rounds * 8 * chunk, TileDesc{-1, 0, 0, 0});
+  for (int s = 0; s < T; ++s) {
+    const int c = s / chunk, pos = s % chunk;
+    const int b = 8 * (chunk * (c / 8) + pos) + (c % 8);
+    plan->tiles[b] = seq[s];
+    grid = std::max(grid, b + 1);
+  }
+  plan->tiles.resize(grid);
+  plan->total_tiles = T;
   return MXMOE_GG_OK;
 }
 
@@ -203,6 +282,40 @@ int check_variant(int variant) {
   if (variant < 0 || variant >= (int)variants().size())
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "variant %d not compiled (have %d)", variant, (int)variants().size());
   return MXMOE_GG_OK;
+}
+
+std::vector<HostProblem> to_host(const mxmoe_gg_problem* problems, int problem_count) {
+  std::vector<HostProblem> hp(problem_count);
+  for (int i = 0; i < problem_count; ++i) {
+    const mxmoe_gg_problem& p = problems[i];
+    hp[i] = HostProblem{p.A,      p.B,      p.scale_a, p.scale_b, p.C,   p.M,   p.N,  p.K,
+                        p.a_bits, p.w_bits, p.gsize,   p.sym,     p.lda, p.ldb, p.ldc};
+  }
+  return hp;
+}
+
+// Host image of the workspace for a plan; pointer columns from `hp` in table-row order.
+std::vector<uint8_t> workspace_image(const Plan& plan, const std::vector<const void*> cols[5], WsLayout* out) {
+  const int P = (int)plan.meta.size();
+  const WsLayout l = ws_layout(P, (int)plan.tiles.size());
+  std::vector<uint8_t> img(l.total, 0);
+  memcpy(img.data(), plan.meta.data(), (size_t)P * sizeof(GGMeta));
+  for (int c = 0; c < 5; ++c) memcpy(img.data() + l.meta + c * l.ptr, cols[c].data(), (size_t)P * sizeof(void*));
+  memcpy(img.data() + l.meta + 5 * l.ptr, plan.tiles.data(), plan.tiles.size() * sizeof(TileDesc));
+  *out = l;
+  return img;
+}
+
+void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe_gg_plan_info* info) {
+  const Variant& v = variants()[variant];
+  info->variant = variant;
+  info->problem_count = (int)plan.meta.size();
+  info->total_tiles = plan.total_tiles;
+  info->grid = (int)plan.tiles.size();
+  info->block = v.threads;
+  info->lds_bytes = v.lds_bytes;
+  info->workspace_bytes = (int64_t)l.total;
+  info->workspace = ws;
 }
 
 }  // namespace
@@ -225,8 +338,11 @@ int mxmoe_gg_list_variants(char* buf, size_t n) {
     for (int q = 0; q < QT_COUNT; ++q) {
       const TileGeom& g = vs[i].geom[q];
       const int bits = q == QT_F16 ? 16 : (q == QT_I8 ? 8 : 4);
-      off += snprintf(line + off, sizeof(line) - off, " %s=TileConfig(BM=%d, BN=%d, BK=%d, WM=%d, WN=%d, WK=1, STAGE=2)",
-                      qnames[q], g.bm, g.bn, g.bkb * 8 / bits, 2, g.threads / 128);
+      const int waves = g.threads / 64;
+      const int wm = 2, wn = waves / wm;
+      off += snprintf(line + off, sizeof(line) - off,
+                      " %s=TileConfig(BM=%d, BN=%d, BK=%d, WM=%d, WN=%d, WK=1, STAGE=2)", qnames[q], g.bm, g.bn,
+                      g.bkb * 8 / bits, wm, wn);
     }
     out += line;
     out += "\n";
@@ -254,9 +370,15 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
   return MXMOE_GG_OK;
 }
 
-int mxmoe_gg_workspace_size(int problem_count, size_t* bytes) {
-  if (problem_count < 0 || !bytes) return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_workspace_size");
-  *bytes = ws_total_bytes(std::max(problem_count, 1));
+int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count, int variant, size_t* bytes) {
+  if (problem_count < 0 || (problem_count > 0 && !problems) || !bytes)
+    return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_workspace_size");
+  int st = check_variant(variant);
+  if (st) return st;
+  Plan plan;
+  st = plan_host(to_host(problems, problem_count), variant, false, &plan);
+  if (st) return st;
+  *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size()).total;
   return MXMOE_GG_OK;
 }
 
@@ -266,50 +388,25 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
     return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_plan");
   int st = check_variant(variant);
   if (st) return st;
-  std::vector<HostProblem> hp(problem_count);
-  for (int i = 0; i < problem_count; ++i) {
-    const mxmoe_gg_problem& p = problems[i];
-    hp[i] = HostProblem{p.A,      p.B,      p.scale_a, p.scale_b, p.C,   p.M,   p.N,  p.K,
-                        p.a_bits, p.w_bits, p.gsize,   p.sym,     p.lda, p.ldb, p.ldc};
-  }
-  std::vector<GGMeta> meta;
-  std::vector<int> order;
-  int total = 0;
-  st = plan_host(hp, variant, true, meta, order, &total);
+  const std::vector<HostProblem> hp = to_host(problems, problem_count);
+  Plan plan;
+  st = plan_host(hp, variant, true, &plan);
   if (st) return st;
-  const int P = (int)meta.size();
-  const size_t need = ws_total_bytes(std::max(P, 1));
-  if (!workspace || workspace_bytes < need)
-    return fail(MXMOE_GG_ERR_WORKSPACE, "workspace too small: need %zu bytes, have %zu", need, workspace_bytes);
-  // host image of the workspace
-  std::vector<uint8_t> img(need, 0);
-  memcpy(img.data(), meta.data(), (size_t)P * sizeof(GGMeta));
-  const size_t mb = ws_meta_bytes(std::max(P, 1)), pb = ws_ptr_bytes(std::max(P, 1));
-  const void** pa = reinterpret_cast<const void**>(img.data() + mb);
-  const void** pbb = reinterpret_cast<const void**>(img.data() + mb + pb);
-  const void** psa = reinterpret_cast<const void**>(img.data() + mb + 2 * pb);
-  const void** psb = reinterpret_cast<const void**>(img.data() + mb + 3 * pb);
-  void** pc = reinterpret_cast<void**>(img.data() + mb + 4 * pb);
-  for (int j = 0; j < P; ++j) {
-    const HostProblem& p = hp[order[j]];
-    pa[j] = p.A;
-    pbb[j] = p.B;
-    psa[j] = p.SA;
-    psb[j] = p.SB;
-    pc[j] = p.C;
+  std::vector<const void*> cols[5];
+  for (int r : plan.order) {
+    cols[0].push_back(hp[r].A);
+    cols[1].push_back(hp[r].B);
+    cols[2].push_back(hp[r].SA);
+    cols[3].push_back(hp[r].SB);
+    cols[4].push_back(hp[r].C);
   }
-  HIP_TRY(hipMemcpyAsync(workspace, img.data(), need, hipMemcpyHostToDevice, (hipStream_t)stream));
-  // the host image is pageable: make sure the runtime has consumed it before it goes away
-  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-  const Variant& v = variants()[variant];
-  info->variant = variant;
-  info->problem_count = P;
-  info->total_tiles = total;
-  info->grid = total;
-  info->block = v.threads;
-  info->lds_bytes = v.lds_bytes;
-  info->workspace_bytes = (int64_t)need;
-  info->workspace = workspace;
+  WsLayout l;
+  std::vector<uint8_t> img = workspace_image(plan, cols, &l);
+  if (!workspace || workspace_bytes < l.total)
+    return fail(MXMOE_GG_ERR_WORKSPACE, "workspace too small: need %zu bytes, have %zu", l.total, workspace_bytes);
+  HIP_TRY(hipMemcpyAsync(workspace, img.data(), l.total, hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // pageable host image must outlive the copy
+  fill_info(plan, variant, l, workspace, info);
   return MXMOE_GG_OK;
 }
 
@@ -319,17 +416,18 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   if (st) return st;
   if (info->total_tiles == 0) return MXMOE_GG_OK;
   const int P = info->problem_count;
+  const WsLayout l = ws_layout(P, info->grid);
   const uint8_t* ws = static_cast<const uint8_t*>(info->workspace);
-  const size_t mb = ws_meta_bytes(std::max(P, 1)), pb = ws_ptr_bytes(std::max(P, 1));
   GGArgs a;
   a.meta = reinterpret_cast<const GGMeta*>(ws);
-  a.ptr_A = reinterpret_cast<const void* const*>(ws + mb);
-  a.ptr_B = reinterpret_cast<const void* const*>(ws + mb + pb);
-  a.ptr_SA = reinterpret_cast<const void* const*>(ws + mb + 2 * pb);
-  a.ptr_SB = reinterpret_cast<const void* const*>(ws + mb + 3 * pb);
-  a.ptr_C = reinterpret_cast<void* const*>(ws + mb + 4 * pb);
+  a.tiles = reinterpret_cast<const TileDesc*>(ws + l.meta + 5 * l.ptr);
+  a.ptr_A = reinterpret_cast<const void* const*>(ws + l.meta);
+  a.ptr_B = reinterpret_cast<const void* const*>(ws + l.meta + l.ptr);
+  a.ptr_SA = reinterpret_cast<const void* const*>(ws + l.meta + 2 * l.ptr);
+  a.ptr_SB = reinterpret_cast<const void* const*>(ws + l.meta + 3 * l.ptr);
+  a.ptr_C = reinterpret_cast<void* const*>(ws + l.meta + 4 * l.ptr);
   a.P = P;
-  a.total_tiles = info->total_tiles;
+  a.n_slots = info->grid;
   variants()[info->variant].launch(a, info->grid, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return MXMOE_GG_OK;
@@ -343,8 +441,8 @@ int mxmoe_gg_run(const mxmoe_gg_problem* problems, int problem_count, int varian
   return mxmoe_gg_launch(&info, stream);
 }
 
-// Reference-compatible entry point (registry.cuh:28-39). The pointer arrays stay on the device
-// and are read by the kernel in place; only the planner table is uploaded.
+// Reference-compatible entry point (registry.cuh:28-39): device pointer arrays, host copies of
+// the sizes and QParams, legacy default stream, per-call planning (as the reference host API).
 int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr_scale_b, void** ptr_Cs,
                     void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
                     mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
@@ -359,71 +457,39 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
   if (problem_count < 0 || !h_problem_sizes || !h_qbits_list)
     return fail(MXMOE_GG_ERR_INVALID, "bad arguments to groupgemm_mxmoe");
   std::vector<HostProblem> hp(problem_count);
-  for (int i = 0; i < problem_count; ++i) {
-    hp[i] = HostProblem{nullptr,
-                        nullptr,
-                        nullptr,
-                        nullptr,
-                        nullptr,
-                        (int)h_problem_sizes[i].x,
-                        (int)h_problem_sizes[i].y,
-                        (int)h_problem_sizes[i].z,
-                        h_qbits_list[i].a_bits,
-                        h_qbits_list[i].w_bits,
-                        h_qbits_list[i].gsize,
-                        h_qbits_list[i].sym,
-                        0,
-                        0,
-                        0};
-  }
-  std::vector<GGMeta> meta;
-  std::vector<int> order;
-  int total = 0;
-  int st = plan_host(hp, kDefaultVariant, false, meta, order, &total);
+  for (int i = 0; i < problem_count; ++i)
+    hp[i] = HostProblem{nullptr, nullptr, nullptr, nullptr, nullptr, (int)h_problem_sizes[i].x,
+                        (int)h_problem_sizes[i].y, (int)h_problem_sizes[i].z, h_qbits_list[i].a_bits,
+                        h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0};
+  Plan plan;
+  int st = plan_host(hp, kDefaultVariant, false, &plan);
   if (st) return st;
-  if (total == 0) return MXMOE_GG_OK;
-  // The kernel indexes pointer arrays by table row, so the caller's arrays can only be used in
-  // place when the planner kept the caller's order; otherwise gather them on the device.
-  const int P = (int)meta.size();
-  const size_t mb = ws_meta_bytes(P), pb = ws_ptr_bytes(P), need = ws_total_bytes(P);
+  if (plan.total_tiles == 0) return MXMOE_GG_OK;
+  // gather the caller's device pointer arrays through the host (same sync cost class as the
+  // reference's per-call cudaMemcpy, kernel_sketch.py:102-104)
+  std::vector<void*> h[5];
+  void** src[5] = {ptr_As, ptr_Bs, ptr_scale_a, ptr_scale_b, ptr_Cs};
+  for (int c = 0; c < 5; ++c) {
+    h[c].resize(problem_count);
+    HIP_TRY(hipMemcpy(h[c].data(), src[c], problem_count * sizeof(void*), hipMemcpyDeviceToHost));
+  }
+  std::vector<const void*> cols[5];
+  for (int r : plan.order)
+    for (int c = 0; c < 5; ++c) cols[c].push_back(h[c][r]);
+  WsLayout l;
+  std::vector<uint8_t> img = workspace_image(plan, cols, &l);
   thread_local void* ws = nullptr;
   thread_local size_t ws_cap = 0;
-  if (ws_cap < need) {
+  if (ws_cap < l.total) {
     if (ws) HIP_TRY(hipFree(ws));
     ws = nullptr;
     ws_cap = 0;
-    HIP_TRY(hipMalloc(&ws, need));
-    ws_cap = need;
+    HIP_TRY(hipMalloc(&ws, l.total));
+    ws_cap = l.total;
   }
-  // gather the caller's device pointer arrays through the host (same sync cost class as the
-  // reference's per-call cudaMemcpy, kernel_sketch.py:102-104)
-  std::vector<void*> hA(problem_count), hB(problem_count), hSA(problem_count), hSB(problem_count), hC(problem_count);
-  HIP_TRY(hipMemcpy(hA.data(), ptr_As, problem_count * sizeof(void*), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(hB.data(), ptr_Bs, problem_count * sizeof(void*), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(hSA.data(), ptr_scale_a, problem_count * sizeof(void*), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(hSB.data(), ptr_scale_b, problem_count * sizeof(void*), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(hC.data(), ptr_Cs, problem_count * sizeof(void*), hipMemcpyDeviceToHost));
-  std::vector<uint8_t> img(need, 0);
-  memcpy(img.data(), meta.data(), (size_t)P * sizeof(GGMeta));
-  for (int j = 0; j < P; ++j) {
-    const int i = order[j];
-    reinterpret_cast<void**>(img.data() + mb)[j] = hA[i];
-    reinterpret_cast<void**>(img.data() + mb + pb)[j] = hB[i];
-    reinterpret_cast<void**>(img.data() + mb + 2 * pb)[j] = hSA[i];
-    reinterpret_cast<void**>(img.data() + mb + 3 * pb)[j] = hSB[i];
-    reinterpret_cast<void**>(img.data() + mb + 4 * pb)[j] = hC[i];
-  }
-  HIP_TRY(hipMemcpy(ws, img.data(), need, hipMemcpyHostToDevice));
-  const Variant& v = variants()[kDefaultVariant];
+  HIP_TRY(hipMemcpy(ws, img.data(), l.total, hipMemcpyHostToDevice));
   mxmoe_gg_plan_info info;
-  info.variant = kDefaultVariant;
-  info.problem_count = P;
-  info.total_tiles = total;
-  info.grid = total;
-  info.block = v.threads;
-  info.lds_bytes = v.lds_bytes;
-  info.workspace_bytes = (int64_t)need;
-  info.workspace = ws;
+  fill_info(plan, kDefaultVariant, l, ws, &info);
   return mxmoe_gg_launch(&info, nullptr);
 }
 

@@ -44,15 +44,25 @@ struct GGMeta {
 };
 static_assert(sizeof(GGMeta) == 64, "GGMeta must stay 64 bytes");
 
+// One output tile (16 B), host-built in dispatch order: tile b is run by workgroup b.
+struct TileDesc {
+  int32_t prob;  // row of the plan table; -1 = empty slot (padding of the XCD interleave)
+  int32_t m0;    // first output row
+  int32_t n0;    // first output column
+  int32_t cls;   // tile-height class (variant specific)
+};
+static_assert(sizeof(TileDesc) == 16, "TileDesc must stay 16 bytes");
+
 struct GGArgs {
   const GGMeta* meta;
+  const TileDesc* tiles;
   const void* const* ptr_A;
   const void* const* ptr_B;
   const void* const* ptr_SA;
   const void* const* ptr_SB;
   void* const* ptr_C;
   int32_t P;
-  int32_t total_tiles;
+  int32_t n_slots;  // gridDim.x
 };
 
 typedef int32_t v2i __attribute__((ext_vector_type(2)));
@@ -118,7 +128,7 @@ struct AccT<QT_F16> {
 template <class Cfg, int QT>
 __device__ __forceinline__ void gg_tile(const GGMeta& mt, const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                         const _Float16* __restrict__ SA, const _Float16* __restrict__ SB,
-                                        _Float16* __restrict__ C, int m_tile, int n_tile, uint8_t* lds) {
+                                        _Float16* __restrict__ C, int m0, int n0, uint8_t* lds) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NT = Cfg::kThreads;
   constexpr int FM = Cfg::FM, FN = Cfg::FN, LA = Cfg::LA, LB = Cfg::LB;
   typedef typename AccT<QT>::type acc_t;
@@ -127,7 +137,6 @@ __device__ __forceinline__ void gg_tile(const GGMeta& mt, const uint8_t* __restr
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
-  const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int rows_a = min(BM, mt.M - m0);
   const int rows_b = min(BN, mt.N - n0);
   const int kbytes = mt.kbytes;
@@ -264,14 +273,14 @@ __device__ __forceinline__ void gg_tile(const GGMeta& mt, const uint8_t* __restr
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int lc = wn * Cfg::WTN + j * 16 + r16;
-      sb[j] = (lc < rows_b) ? SB[n0 + lc] : (_Float16)0;
+      sb[j] = SB[n0 + min(lc, rows_b - 1)];
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int lr = wm * Cfg::WTM + i * 16 + 4 * g + r;
-        const _Float16 sa = (lr < rows_a) ? SA[m0 + lr] : (_Float16)0;
+        const _Float16 sa = SA[m0 + min(lr, rows_a - 1)];
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int lc = wn * Cfg::WTN + j * 16 + r16;
@@ -312,18 +321,11 @@ struct FusedCfg {
 template <class C16, class C8, class C4>
 __global__ __launch_bounds__(C16::kThreads, C16::kMinWavesPerEU) void gg_fused_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[FusedCfg<C16, C8, C4>::LDS_BYTES];
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  if (t >= args.total_tiles) return;
-  // binary search: last problem with tile_begin <= t (empty problems are never planned)
-  int lo = 0, hi = args.P - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (args.meta[mid].tile_begin <= t) lo = mid;
-    else hi = mid - 1;
-  }
+  const TileDesc td = args.tiles[blockIdx.x];
+  if (td.prob < 0) return;
+  const int lo = td.prob;
   const GGMeta mt = args.meta[lo];
-  const int local = t - mt.tile_begin;
-  const int m_tile = local / mt.tiles_n, n_tile = local - m_tile * mt.tiles_n;
+  const int m_tile = td.m0, n_tile = td.n0;
   const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[lo]);
   const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[lo]);
   _Float16* C = static_cast<_Float16*>(args.ptr_C[lo]);
@@ -335,6 +337,228 @@ __global__ __launch_bounds__(C16::kThreads, C16::kMinWavesPerEU) void gg_fused_k
                        static_cast<const _Float16*>(args.ptr_SB[lo]), C, m_tile, n_tile, lds);
   } else {
     gg_tile<C16, QT_F16>(mt, A, B, nullptr, nullptr, C, m_tile, n_tile, lds);
+  }
+}
+
+
+// ============================================================================================
+// v2: 512-thread workgroups (8 waves, 2M x 4N), BN = 256, tile height class BM in {256, 128}.
+//   * global -> LDS by LDS-DMA (global_load_lds_dwordx4): one wave-instruction fills 8 rows x
+//     128 B of the lane-linear LDS image; the (row>>1)&7 chunk swizzle is applied on the SOURCE
+//     address (a lane of LDS slot p of row r loads logical chunk p ^ swz(r)), the reads apply the
+//     same XOR — both sides or neither (cdna_hip_programming.md rule 21);
+//   * rows past M / N are clamped to the last valid row (their outputs are never stored), so no
+//     load is predicated; K must be a multiple of the 128-B stage (the planner checks);
+//   * two LDS stages; stage s+1 is in flight (LDS-DMA) while stage s feeds the MFMAs;
+//   * MFMA operands swapped (src0 = B fragment, src1 = A fragment): each lane then owns 4
+//     consecutive output COLUMNS of one row, packed into one 8-B LDS write in the epilogue;
+//   * epilogue: each wave stages its own fp16 sub-tile in LDS (XOR-swizzled 16-B chunks) and
+//     stores full 128-B row segments with 16-B stores.
+// ============================================================================================
+template <int BM_>
+struct V2Cfg {
+  static constexpr int BM = BM_, BN = 256, NT = 512, BKB = 128;
+  static constexpr int WM = 2, WN = 4;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB, STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int GA = BM / 64, GB = BN / 64;  // LDS-DMA wave-instructions per wave per stage
+  static constexpr int EPI_BYTES = WM * WN * WTM * WTN * 2;
+  static constexpr int LDS_BYTES = 2 * STAGE_BYTES > EPI_BYTES ? 2 * STAGE_BYTES : EPI_BYTES;
+  static_assert(WTN == 64, "epilogue assumes 128-B staged rows");
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
+}
+
+template <class Cfg, int QT>
+__device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __restrict__ A,
+                                           const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
+                                           const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
+                                           uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
+  typedef typename AccT<QT>::type acc_t;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N, kbytes = mt.kbytes;
+  const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
+  const int nst = kbytes / Cfg::BKB;
+
+  // per-lane LDS-DMA sources (row clamped, chunk pre-swizzled); + kb per stage
+  const uint8_t* srcA[GA];
+  const uint8_t* srcB[GB];
+  {
+    const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int row = (wave * GA + j) * 8 + rsub;
+      const int grow = min(m0 + row, M - 1);
+      srcA[j] = A + (int64_t)grow * lda + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = (wave * GB + j) * 8 + rsub;
+      const int grow = min(n0 + row, N - 1);
+      srcB[j] = B + (int64_t)grow * ldb + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+  }
+  auto issue = [&](int s, int buf) {
+    uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
+    uint8_t* Bs = As + Cfg::A_BYTES;
+    const int kb = s * Cfg::BKB;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
+  };
+
+  acc_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+
+  const int swz = (r16 >> 1) & 7;  // rows of a fragment are base + r16 with base % 16 == 0
+  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
+  const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
+    const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
+    if constexpr (QT == QT_I4) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
+        v4i a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        const uint32_t off = (uint32_t)(((kc * 4 + g) ^ swz) << 4);
+        if constexpr (QT == QT_I8) {
+          v4i a[FM], b[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v4i*>(As + i * 2048 + off);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v4i*>(Bs + j * 2048 + off);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+        } else {
+          v8h a[FM], b[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v8h*>(Bs + j * 2048 + off);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- mainloop: stage s+1 in flight (LDS-DMA) while stage s is consumed ----
+  if (nst > 0) {
+    issue(0, 0);
+    __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
+    for (int s = 0; s < nst; ++s) {
+      if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
+      compute(s & 1);
+      __syncthreads();  // own LDS-DMA landed (vmcnt(0)); every wave done reading buffer s&1
+    }
+  }
+
+  // ---- epilogue: per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
+  uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
+  const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
+  _Float16 sa[FM];
+  _Float16 sb[FN][4];
+  if constexpr (QT != QT_F16) {
+    // indices clamped (not predicated: a guarded load per element becomes a branch + wait each);
+    // values of rows / columns past M / N are never stored
+#pragma unroll
+    for (int i = 0; i < FM; ++i) sa[i] = SA[min(mrow0 + i * 16 + r16, M - 1)];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = min(ncol0 + j * 16 + 4 * g, N - 4);  // N % 8 == 0: a group of 4 is all in or all out
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sb[j][r] = SB[n + r];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = i * 16 + r16;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      _Float16 h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (QT == QT_F16) {
+          h[r] = (_Float16)acc[i][j][r];
+        } else {
+          constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
+          const _Float16 s16 = sa[i] * sb[j][r];
+          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
+          asm volatile("" : "+v"(prod));  // keep the f32 rounding of the product (see gg_tile)
+          h[r] = (_Float16)(0.0f + prod);
+        }
+      }
+      const int q = 2 * j + (g >> 1);
+      uint2 pk;
+      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
+      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
+      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
+    }
+  }
+  // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
+#pragma unroll 4
+  for (int it = 0; it < Cfg::WTM / 8; ++it) {
+    const int row = it * 8 + (lane >> 3), q = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
+    const int m = mrow0 + row, n = ncol0 + q * 8;
+    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+  }
+}
+
+// v2 fused kernel: qtype x height-class dispatch, uniform per workgroup.
+__global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
+  const TileDesc td = args.tiles[blockIdx.x];
+  if (td.prob < 0) return;
+  const GGMeta mt = args.meta[td.prob];
+  const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[td.prob]);
+  const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[td.prob]);
+  const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
+  const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
+  _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
+  const bool tall = td.cls == 0;
+  if (mt.qtype == QT_I8) {
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if (mt.qtype == QT_I4) {
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else {
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   }
 }
 

@@ -123,7 +123,7 @@ class GroupGemm:
                     raise ValueError(f"all tensors must live on {device}, got {t.device}")
         P = len(self.problems)
         self._c_problems = (nat.GGProblemC * max(P, 1))(*[p.to_c() for p in self.problems])
-        ws_bytes = nat.workspace_size(P)
+        ws_bytes = nat.workspace_size(self._c_problems, P, self.variant)
         self.workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
         self.info = nat.GGPlanInfo()
         nat.check(nat.lib().mxmoe_gg_plan(self._c_problems, P, self.variant, ctypes.c_void_p(self.workspace.data_ptr()),

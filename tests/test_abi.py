@@ -49,8 +49,15 @@ def test_abi_version_and_variants():
     assert t["BM"] > 0 and t["BN"] > 0 and t["threads"] % 64 == 0
 
 
-def test_workspace_size_monotone():
-    assert nat.workspace_size(1) <= nat.workspace_size(61) <= nat.workspace_size(1000)
+def test_workspace_size_grows_with_tiles():
+    def ws(ps, v=0):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.workspace_size(arr, len(ps), v)
+
+    small = ws([_prob(M=64)])
+    big = ws([_prob(M=8192, N=4096)])
+    assert 0 < small < big
+    assert ws([_prob(M=0)]) > 0  # empty problems plan to an empty tile table
 
 
 def _plan(problems, ws_bytes=1 << 20):

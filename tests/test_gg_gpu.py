@@ -37,20 +37,31 @@ def _gpu():
     nat.lib()
 
 
-@pytest.mark.parametrize("variant", range(3))
+NV = 4  # compiled variants (tests/test_abi checks the count)
+
+
+def _kbytes_ok(variant, K, q):
+    bits = 16 if not q.is_quant else q.a_bits
+    return variant < 3 or (K * bits // 8) % 128 == 0  # v2 stages whole 128-B K slices
+
+
+@pytest.mark.parametrize("variant", range(NV))
 @pytest.mark.parametrize("q", [FP16, W8A8, W4A4], ids=["fp16", "w8a8", "w4a4"])
 def test_single_qtype_edge_shapes(q, variant):
-    shapes = [(1, 128, 256), (17, 256, 128), (130, 128, 384), (257, 136, 512), (64, 8, 1024)]
+    shapes = [(1, 128, 256), (17, 256, 128), (130, 128, 384), (257, 136, 512), (64, 8, 1024), (300, 520, 512),
+              (513, 264, 256)]
+    shapes = [s for s in shapes if _kbytes_ok(variant, s[2], q)]
     hps = [HostProblem(M, N, K, q, seed=100 + i, device=DEV) for i, (M, N, K) in enumerate(shapes)]
     group_gemm([h.problem for h in hps], variant=variant)
     torch.cuda.synchronize()
     _check(hps)
 
 
-@pytest.mark.parametrize("variant", range(3))
+@pytest.mark.parametrize("variant", range(NV))
 def test_mixed_fused_launch(variant):
     specs = [(300, 256, 256, W8A8), (0, 256, 256, W4A4), (129, 384, 512, W4A4), (77, 128, 192, FP16),
-             (513, 256, 128, W8A8), (5, 128, 64, W4A4), (256, 256, 256, FP16)]
+             (513, 256, 128, W8A8), (5, 128, 64, W4A4), (256, 256, 256, FP16), (384, 512, 1024, W8A8)]
+    specs = [s for s in specs if _kbytes_ok(variant, s[2], s[3])]
     hps = [HostProblem(M, N, K, q, seed=7 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)
     gg.launch()
@@ -64,6 +75,7 @@ def test_mixed_fused_launch(variant):
 
 @pytest.mark.parametrize("q", [W8A8, W4A4, FP16], ids=["w8a8", "w4a4", "fp16"])
 def test_k_tail_inside_stage(q):
+    # (v0 variants; the v2 planner rejects K tails: see test_v2_rejects_k_tail)
     # K bytes not a multiple of the 128-B stage: zero-filled tail must not change the sum
     bits = 16 if not q.is_quant else q.a_bits
     K = (128 * 8 // bits) * 3 + (128 // bits)  # 3 full stages + 16 bytes
@@ -73,13 +85,14 @@ def test_k_tail_inside_stage(q):
     _check(hps)
 
 
-def test_strided_c_nslices():
+@pytest.mark.parametrize("variant", range(NV))
+def test_strided_c_nslices(variant):
     # two N-slices of one logical problem written into one C buffer with ldc = N_total
     M, N, K = 200, 512, 256
     C = torch.full((M, N), float("nan"), dtype=torch.float16, device=DEV)
     h0 = HostProblem(M, 256, K, W8A8, seed=11, device=DEV, C=C, c_col0=0)
     h1 = HostProblem(M, 256, K, W8A8, seed=12, device=DEV, C=C, c_col0=256)
-    group_gemm([h0.problem, h1.problem])
+    group_gemm([h0.problem, h1.problem], variant=variant)
     torch.cuda.synchronize()
     full = C.cpu().numpy()
     assert (full[:, :256].view(np.uint16) == h0.expected().view(np.uint16)).all()
@@ -111,9 +124,10 @@ def test_unsupported_qtype_raises():
         group_gemm([p])
 
 
-def test_graph_capture_replay():
+@pytest.mark.parametrize("variant", [0, 3])
+def test_graph_capture_replay(variant):
     hps = [HostProblem(150, 256, 512, W8A8, seed=31, device=DEV), HostProblem(90, 128, 256, W4A4, seed=32, device=DEV)]
-    gg = GroupGemm([h.problem for h in hps])
+    gg = GroupGemm([h.problem for h in hps], variant=variant)
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -124,3 +138,9 @@ def test_graph_capture_replay():
     g.replay()
     torch.cuda.synchronize()
     _check(hps)
+
+
+def test_v2_rejects_k_tail():
+    h = HostProblem(70, 128, 16 * 9, W8A8, seed=3, device=DEV)
+    with pytest.raises(nat.GGError, match="multiple of 128 bytes"):
+        group_gemm([h.problem], variant=3)
