@@ -96,7 +96,7 @@ Variant make_v2(const char* name) {
   v.threads = 512;
   v.lds_bytes = V2Cfg<256>::LDS_BYTES;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
-  v.k_stage_bytes = 128;
+  v.k_stage_bytes = 0;  // K tails handled in-kernel (last stage)
   v.tail_bm = 128;
   v.launch = &launch_v2;
   return v;

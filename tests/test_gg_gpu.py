@@ -41,8 +41,7 @@ NV = 4  # compiled variants (tests/test_abi checks the count)
 
 
 def _kbytes_ok(variant, K, q):
-    bits = 16 if not q.is_quant else q.a_bits
-    return variant < 3 or (K * bits // 8) % 128 == 0  # v2 stages whole 128-B K slices
+    return True  # every variant handles K tails (multiples of 16 bytes)
 
 
 @pytest.mark.parametrize("variant", range(NV))
@@ -73,14 +72,14 @@ def test_mixed_fused_launch(variant):
     _check(hps)
 
 
+@pytest.mark.parametrize("variant", range(NV))
 @pytest.mark.parametrize("q", [W8A8, W4A4, FP16], ids=["w8a8", "w4a4", "fp16"])
-def test_k_tail_inside_stage(q):
-    # (v0 variants; the v2 planner rejects K tails: see test_v2_rejects_k_tail)
-    # K bytes not a multiple of the 128-B stage: zero-filled tail must not change the sum
+def test_k_tail_inside_stage(q, variant):
+    # K bytes not a multiple of the 128-B stage: the tail must not change the sum
     bits = 16 if not q.is_quant else q.a_bits
-    K = (128 * 8 // bits) * 3 + (128 // bits)  # 3 full stages + 16 bytes
-    hps = [HostProblem(70, 128, K, q, seed=3, device=DEV)]
-    group_gemm([h.problem for h in hps])
+    hps = [HostProblem(70 + 61 * t, 128 + 8 * t, (128 * 8 // bits) * 3 + (128 // bits) * t, q, seed=3 + t, device=DEV)
+           for t in range(1, 8)]  # 3 full stages + 16..112 bytes
+    group_gemm([h.problem for h in hps], variant=variant)
     torch.cuda.synchronize()
     _check(hps)
 
@@ -139,8 +138,3 @@ def test_graph_capture_replay(variant):
     torch.cuda.synchronize()
     _check(hps)
 
-
-def test_v2_rejects_k_tail():
-    h = HostProblem(70, 128, 16 * 9, W8A8, seed=3, device=DEV)
-    with pytest.raises(nat.GGError, match="multiple of 128 bytes"):
-        group_gemm([h.problem], variant=3)

@@ -65,9 +65,6 @@ def _verify(probs, exp):
 @pytest.mark.parametrize("variant", range(4))
 def test_golden_vectors(name, variant):
     probs, exp = _load(name)
-    if variant == 3:  # v2 needs whole 128-B K slices
-        keep = [i for i, p in enumerate(probs) if (p.K * (16 if not p.q.is_quant else p.q.a_bits) // 8) % 128 == 0]
-        probs, exp = [probs[i] for i in keep], [exp[i] for i in keep]
     group_gemm(probs, variant=variant)
     torch.cuda.synchronize()
     _verify(probs, exp)
