@@ -1,0 +1,47 @@
+"""Launch one GroupGEMM call repeatedly (for rocprofv3 counter runs / A-B of variants).
+
+python tools/kbench.py --cfg w8a8 --gg gate_up --variants 0,3 --iters 20 [--only shared|routed|all]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from mxmoe_amd.groupgemm import GroupGemm  # noqa: E402
+from mxmoe_amd.harness import build_layer_inputs, time_launches  # noqa: E402
+from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", default="w8a8")
+    ap.add_argument("--gg", default="gate_up")
+    ap.add_argument("--variants", default="0,3")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="all", choices=["all", "shared", "routed"])
+    args = ap.parse_args()
+    kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
+          "mixed": dict(qconfig=mixed_qconfig_lp1())}[args.cfg]
+    shapes = load_workload(qwen2_layer11_workload(8192, **kw))["layer-11"][args.gg]
+    if args.only == "shared":
+        shapes = shapes[-1:]
+    elif args.only == "routed":
+        shapes = shapes[:-1]
+    inp = build_layer_inputs(shapes)
+    for v in [int(x) for x in args.variants.split(",")]:
+        gg = GroupGemm(inp.problems, variant=v)
+        t = time_launches(gg.launch, warmup=3, iters=args.iters)
+        print(json.dumps({"variant": v, "cfg": args.cfg, "gg": args.gg, "only": args.only,
+                          "median_ms": round(t["median_ms"], 4), "tiles": gg.total_tiles, "grid": gg.info.grid,
+                          "tflops": round(inp.flops / (t["median_ms"] * 1e-3) / 1e12, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
