@@ -373,6 +373,10 @@ struct V2Cfg {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
+// 16 zero bytes in global memory: the LDS-DMA source of K-tail chunks (they land as zeros in LDS,
+// so the MFMA loop needs no tail code and no extra registers).
+__device__ __attribute__((aligned(16))) const uint32_t g_zero16[4] = {0, 0, 0, 0};
+
 __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
@@ -420,18 +424,18 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
       for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
     } else {
-      // K tail: chunks past K re-read the stage's first chunk (stays inside the row); their
-      // products are zeroed in registers by the TAIL compute
+      // K tail (last stage only): chunks past K load 16 zero bytes instead
       const int rsub = lane >> 3, p = lane & 7;
+      const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
 #pragma unroll
       for (int j = 0; j < GA; ++j) {
         const int kc = (p ^ ((((wave * GA + j) * 8 + rsub) >> 1) & 7)) << 4;
-        glds16(srcA[j] + kb - (kb + kc >= kbytes ? kc : 0), As + (wave * GA + j) * 1024);
+        glds16(kb + kc < kbytes ? srcA[j] + kb : zero, As + (wave * GA + j) * 1024);
       }
 #pragma unroll
       for (int j = 0; j < GB; ++j) {
         const int kc = (p ^ ((((wave * GB + j) * 8 + rsub) >> 1) & 7)) << 4;
-        glds16(srcB[j] + kb - (kb + kc >= kbytes ? kc : 0), Bs + (wave * GB + j) * 1024);
+        glds16(kb + kc < kbytes ? srcB[j] + kb : zero, Bs + (wave * GB + j) * 1024);
       }
     }
   };
@@ -445,24 +449,18 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   const int swz = (r16 >> 1) & 7;  // rows of a fragment are base + r16 with base % 16 == 0
   const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
-  // TAIL: only the first kvalid bytes of this stage are inside K; B fragments past it are zeroed
-  auto compute = [&](int buf, auto tail_tag, int kvalid) {
-    constexpr bool TAIL = decltype(tail_tag)::value;
+  auto compute = [&](int buf) {
     const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
     const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
     if constexpr (QT == QT_I4) {
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
-        const bool kin = !TAIL || (st * 32 + g * 8 < kvalid);
         v4i a[FM], b[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off));
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off));
-          if constexpr (TAIL) b[j] = kin ? b[j] : v4i{0, 0, 0, 0};
-        }
+        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off));
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -472,16 +470,12 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc) {
         const uint32_t off = (uint32_t)(((kc * 4 + g) ^ swz) << 4);
-        const bool kin = !TAIL || (kc * 64 + g * 16 < kvalid);
         if constexpr (QT == QT_I8) {
           v4i a[FM], b[FN];
 #pragma unroll
           for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v4i*>(As + i * 2048 + off);
 #pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            b[j] = *reinterpret_cast<const v4i*>(Bs + j * 2048 + off);
-            if constexpr (TAIL) b[j] = kin ? b[j] : v4i{0, 0, 0, 0};
-          }
+          for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v4i*>(Bs + j * 2048 + off);
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -492,10 +486,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
           for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
 #pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            b[j] = *reinterpret_cast<const v8h*>(Bs + j * 2048 + off);
-            if constexpr (TAIL) b[j] = kin ? b[j] : v8h{0, 0, 0, 0, 0, 0, 0, 0};
-          }
+          for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v8h*>(Bs + j * 2048 + off);
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -512,9 +503,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
     for (int s = 0; s < nst; ++s) {
       if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
-      const int kvalid = kbytes - s * Cfg::BKB;
-      if (kvalid >= Cfg::BKB) compute(s & 1, std::false_type{}, Cfg::BKB);
-      else compute(s & 1, std::true_type{}, kvalid);
+      compute(s & 1);
       __syncthreads();  // own LDS-DMA landed (vmcnt(0)); every wave done reading buffer s&1
     }
   }

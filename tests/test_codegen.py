@@ -1,0 +1,43 @@
+"""Codegen guards (CPU, hipcc cross-compile): no kernel may use scratch (private segment), and the
+VGPR count must leave the occupancy the variant was designed for (cdna_hip_programming.md rule 20)."""
+from __future__ import annotations
+
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from mxmoe_amd import build as b
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    out = tmp_path_factory.mktemp("asm") / "gg.s"
+    cmd = [b.HIPCC, "-O3", "-std=c++17", f"--offload-arch={b.ARCH}", "--cuda-device-only", "-S", "-o", str(out),
+           "-I", str(b.ROOT / "include"), str(b.SOURCES[0])]
+    subprocess.run(cmd, check=True, capture_output=True)
+    return out.read_text()
+
+
+def _kernels(asm):
+    ks = {}
+    for m in re.finditer(r"\.private_segment_fixed_size: (\d+)\n\s+\.sgpr_count:\s+\d+\n\s+\.sgpr_spill_count: (\d+)\n"
+                         r"\s+\.symbol:\s+(\S+)\.kd\n(?:.*\n){0,12}?\s+\.vgpr_count:\s+(\d+)\n\s+\.vgpr_spill_count: (\d+)",
+                         asm):
+        ks[m.group(3)] = dict(private=int(m.group(1)), sgpr_spill=int(m.group(2)), vgpr=int(m.group(4)),
+                              vgpr_spill=int(m.group(5)))
+    return ks
+
+
+def test_no_scratch_no_spills(asm):
+    ks = _kernels(asm)
+    assert len(ks) >= 4
+    for name, k in ks.items():
+        assert k["private"] == 0 and k["vgpr_spill"] == 0 and k["sgpr_spill"] == 0, (name, k)
+
+
+def test_v2_keeps_two_waves_per_simd(asm):
+    ks = _kernels(asm)
+    v2 = [k for n, k in ks.items() if "gg_v2_kernel" in n]
+    assert v2 and v2[0]["vgpr"] <= 256  # 8-wave workgroup = 2 waves/SIMD needs <= 256 VGPRs
