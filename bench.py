@@ -268,7 +268,9 @@ def main():
 
 
 def default_variant(cfg: str) -> int:
-    return 0
+    from mxmoe_amd import _native as nat
+
+    return nat.default_variant()
 
 
 if __name__ == "__main__":

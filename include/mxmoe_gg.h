@@ -94,6 +94,9 @@ const char* mxmoe_gg_last_error(void);
 /* Number of compiled kernel variants. */
 int mxmoe_gg_variant_count(void);
 
+/* The variant used when the caller has no preference (and by groupgemm_mxmoe). */
+int mxmoe_gg_default_variant(void);
+
 /* Writes a newline-separated description of every compiled variant into buf (truncated,
  * always NUL-terminated when n > 0). Line i describes variant i in the reference TileConfig
  * repr form per qcfg, e.g. "0 fused fp16=TileConfig(BM=128, BN=128, ...) w8a8_g-1_sym=...".

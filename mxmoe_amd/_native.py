@@ -68,7 +68,8 @@ class GGPlanInfo(ctypes.Structure):
 
 # every symbol include/mxmoe_gg.h declares (tests check the .so exports exactly these)
 EXPORTED_SYMBOLS = (
-    "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_list_variants",
+    "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
+    "mxmoe_gg_list_variants",
     "mxmoe_gg_variant_tile", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
     "groupgemm_mxmoe",
 )
@@ -84,6 +85,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_last_error.argtypes = []
     lib.mxmoe_gg_variant_count.restype = c.c_int
     lib.mxmoe_gg_variant_count.argtypes = []
+    lib.mxmoe_gg_default_variant.restype = c.c_int
+    lib.mxmoe_gg_default_variant.argtypes = []
     lib.mxmoe_gg_list_variants.restype = c.c_int
     lib.mxmoe_gg_list_variants.argtypes = [c.c_char_p, c.c_size_t]
     lib.mxmoe_gg_variant_tile.restype = c.c_int
@@ -127,6 +130,10 @@ def check(status: int) -> None:
 
 def variant_count() -> int:
     return lib().mxmoe_gg_variant_count()
+
+
+def default_variant() -> int:
+    return lib().mxmoe_gg_default_variant()
 
 
 def list_variants() -> list[str]:

@@ -116,7 +116,7 @@ const std::vector<Variant>& variants() {
   return v;
 }
 
-constexpr int kDefaultVariant = 0;
+constexpr int kDefaultVariant = 3;  // v2 (fastest on every qwen2_moe layer-11 config)
 
 int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
   if (a_bits == 16 && w_bits == 16) {
@@ -327,6 +327,8 @@ int mxmoe_gg_abi_version(void) { return MXMOE_GG_ABI_VERSION; }
 const char* mxmoe_gg_last_error(void) { return g_last_error.c_str(); }
 
 int mxmoe_gg_variant_count(void) { return (int)variants().size(); }
+
+int mxmoe_gg_default_variant(void) { return kDefaultVariant; }
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
   static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym"};

@@ -110,10 +110,10 @@ class GroupGemm:
     allocation and no host synchronisation, so it can be captured in a CUDA/HIP graph.
     """
 
-    def __init__(self, problems: Sequence[Problem], variant: int = 0, device: Optional[torch.device] = None,
-                 stream: Optional[torch.cuda.Stream] = None):
+    def __init__(self, problems: Sequence[Problem], variant: Optional[int] = None,
+                 device: Optional[torch.device] = None, stream: Optional[torch.cuda.Stream] = None):
         self.problems = list(problems)
-        self.variant = int(variant)
+        self.variant = nat.default_variant() if variant is None else int(variant)
         if device is None:
             device = self.problems[0].C.device if self.problems else torch.device("cuda")
         self.device = device
@@ -143,7 +143,8 @@ class GroupGemm:
     __call__ = launch
 
 
-def group_gemm(problems: Sequence[Problem], variant: int = 0, stream: Optional[torch.cuda.Stream] = None) -> None:
+def group_gemm(problems: Sequence[Problem], variant: Optional[int] = None,
+               stream: Optional[torch.cuda.Stream] = None) -> None:
     """Plan + launch once (the reference host API's per-call behaviour)."""
     GroupGemm(problems, variant=variant, stream=stream).launch(stream)
 

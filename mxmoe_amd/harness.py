@@ -86,7 +86,7 @@ def time_launches(fn, warmup: int = 20, iters: int = 50, stream: Optional[torch.
     return {"median_ms": statistics.median(ts), "mean_ms": sum(ts) / len(ts), "min_ms": min(ts), "iters": iters}
 
 
-def bench_call(inputs: LayerInputs, variant: int = 0, warmup: int = 20, iters: int = 50) -> dict:
+def bench_call(inputs: LayerInputs, variant: Optional[int] = None, warmup: int = 20, iters: int = 50) -> dict:
     gg = GroupGemm(inputs.problems, variant=variant)
     t = time_launches(gg.launch, warmup, iters)
     t["tflops"] = inputs.flops / (t["median_ms"] * 1e-3) / 1e12
