@@ -106,10 +106,11 @@ def cpu_baseline(cfg: str, shapes, budget_s: float = 15.0) -> dict:
         names.append(f"{gg}[{M}x{N}x{K} {s.qcfg}]")
         if t_used > budget_s:
             break
+    shown = ", ".join(names[:3]) + (f", ... ({len(names) - 3} more)" if len(names) > 3 else "")
     return {"value": round(done_flops / t_used / 1e12, 6), "unit": "TFLOP/s", "cores": threads, "kind": "port",
-            "sample": f"{len(names)} routed-expert problems of the same layer ({', '.join(names)}), "
-                      f"{done_flops / 1e9:.1f} GFLOP in {t_used:.1f} s; oracle/gg_oracle.c (OpenMP, "
-                      f"{platform.processor() or platform.machine()})"}
+            "sample": f"first {len(names)} routed-expert problems of the same layer in call order ({shown}); "
+                      f"{done_flops / 1e9:.1f} GFLOP in {t_used:.1f} s; oracle/gg_oracle.c, OpenMP "
+                      f"{threads} threads, {platform.machine()}"}
 
 
 def load_pmc_traffic(cfg: str):
@@ -257,7 +258,8 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4),
                          "traffic": pmc.get("hbm_bytes_per_step") if isinstance(pmc, dict) else None,
-                         "kernel": "mxmoe::gg_fused_kernel (gate_up + down launches)",
+                         "kernel": ("mxmoe::gg_v2_kernel" if main_res["variant"] == 3 else "mxmoe::gg_fused_kernel")
+                         + " (gate_up + down launches; achieved = sum FLOPs / sum mean launch time)",
                          "launch_ms": {"gate_up": round(t_gu, 4), "down": round(t_dn, 4)}},
             "cpu_baseline": cpu,
             "extras": extras,
