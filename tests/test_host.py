@@ -103,3 +103,21 @@ def test_qcfg_info():
     assert tc.get_info_from_qcfg_str("w8a8_g-1_sym") == (8, 8, -1, True)
     assert tc.get_info_from_qcfg_str("w4a16_g128_asym") == (4, 16, 128, False)
     assert set(tc.MI355X_QCFG) <= set(tc.SUPPORTED_QCFG)
+
+
+def test_cli_workload_step(tmp_path, monkeypatch):
+    import run_mxmoe_gg as cli
+
+    class A:
+        qconfig = str(wl.WORKLOAD_DIR / "qconfig_qwen2_moe_w4a4+w8a8_wbits5.0_lp1.json")
+        qstr = None
+        layer = 11
+
+    suffix, kw, qcfgs = cli.workload_suffix(A)
+    assert suffix == "-5.0_lp1.json" and qcfgs == ["w4a4_g-1_sym", "w8a8_g-1_sym"] and "qconfig" in kw
+    A.qconfig, A.qstr = None, "w8a8_g-1_sym"
+    assert cli.workload_suffix(A)[0] == "-w8a8_g-1_sym.json"
+    A.qstr = None
+    assert cli.workload_suffix(A)[0] == "-fp16.json"
+    t = cli.find_trace("qwen2_moe", "wiki2", 11, None)
+    assert t["topk"] == 4 and len(t["layer-11"]["access_freq"]) == 60 and len([k for k in t if k.startswith("layer-")]) == 24
