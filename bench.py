@@ -46,34 +46,15 @@ def log(*a):
 
 
 def layer_shapes(cfg: str, world: int, rank: int, bs: int = 8192):
-    """Per-rank problem lists {gate_up, down} (expert-parallel weak scaling, see module doc)."""
-    from mxmoe_amd.workload import QShape, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+    """Per-rank problem lists {gate_up, down} (expert-parallel weak scaling, mxmoe_amd/dist.py)."""
+    from mxmoe_amd.dist import ep_shard
+    from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
 
     kw = CONFIGS[cfg]["kw"]
     if kw == "mixed":
         kw = dict(qconfig=mixed_qconfig_lp1())
     wl = load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
-    if world == 1:
-        return wl
-    routed = list(range(len(wl["gate_up"]) - 1))
-    # LPT: heaviest expert (gate_up+down FLOPs at global M) to the least-loaded rank
-    cost = {e: wl["gate_up"][e].flops + wl["down"][e].flops for e in routed}
-    load = [0] * world
-    owner = {}
-    for e in sorted(routed, key=lambda e: -cost[e]):
-        r = min(range(world), key=lambda r: load[r])
-        owner[e] = r
-        load[r] += cost[e]
-    out = {}
-    for gg in ("gate_up", "down"):
-        lst = []
-        for e in routed:
-            if owner[e] == rank:
-                s = wl[gg][e]
-                lst.append(QShape([s.M * world, s.N, s.K], s.w_bits, s.a_bits, s.gsize, s.sym))
-        lst.append(wl[gg][-1])  # shared expert, local tokens
-        out[gg] = lst
-    return out
+    return ep_shard(wl, world, rank)
 
 
 def cpu_baseline(cfg: str, shapes, budget_s: float = 15.0) -> dict:

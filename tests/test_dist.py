@@ -1,0 +1,105 @@
+"""Multi-process (gloo, world_size 2 and 4, CPU) tests of the multi-GPU partitioning + exchange."""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mxmoe_amd.dist import allgather_outputs, ep_shard, lpt_assign, nslice_plan
+from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
+
+
+def _layer():
+    return load_workload(qwen2_layer11_workload(8192, qstr="w8a8_g-1_sym"))["layer-11"]
+
+
+def test_lpt_balance():
+    owner = lpt_assign([10, 9, 8, 7, 6, 5, 4], 3)
+    loads = [sum(c for c, o in zip([10, 9, 8, 7, 6, 5, 4], owner) if o == r) for r in range(3)]
+    assert max(loads) - min(loads) <= 4
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ep_shard_covers_each_expert_once(world):
+    layer = _layer()
+    seen = []
+    per_rank = []
+    for r in range(world):
+        sh = ep_shard(layer, world, r)
+        assert sh["gate_up"][-1].M == 8192  # replicated shared expert on local tokens
+        per_rank.append(sum(p.flops for gg in sh for p in sh[gg]))
+        seen += [p.N for p in sh["gate_up"][:-1]]
+    assert len(seen) == 60
+    single = sum(p.flops for gg in layer for p in layer[gg])
+    assert max(per_rank) < 1.06 * single  # weak scaling: ~one layer of work per rank
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_nslice_plan_splits_shared_expert(world):
+    layer = _layer()["gate_up"]
+    plan = nslice_plan(layer, world)
+    covered = {}
+    for work in plan:
+        for w in work:
+            covered.setdefault(w.problem, []).append((w.n0, w.n1))
+    for i, s in enumerate(layer):
+        spans = sorted(covered[i])
+        assert spans[0][0] == 0 and spans[-1][1] == s.N
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert all((n1 - n0) % 256 == 0 or n1 == s.N for n0, n1 in spans)
+    loads = [sum(2 * layer[w.problem].M * w.width * layer[w.problem].K for w in work) for work in plan]
+    assert max(loads) / (sum(loads) / world) < 1.15  # the shared expert no longer caps the speedup at 2x
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mxmoe_amd.workload import QShape
+
+        shapes = [QShape([37, 512, 64]), QShape([5, 256, 64]), QShape([64, 1024, 64]), QShape([0, 256, 64])]
+        plan = nslice_plan(shapes, world, slice_n=256, target_frac=0.3)
+        # each rank "computes" its slices: value = 1000*problem + column, packed in work order
+        parts = []
+        for w in plan[rank]:
+            M = shapes[w.problem].M
+            cols = torch.arange(w.n0, w.n1, dtype=torch.float32)
+            parts.append((1000.0 * w.problem + cols).expand(M, -1).reshape(-1))
+        local = torch.cat(parts) if parts else torch.zeros(0)
+        outs = [torch.full((max(s.M, 1), s.N), -1.0) for s in shapes]
+        allgather_outputs(shapes, plan, local, outs)
+        ok = all(torch.equal(outs[i][: s.M], (1000.0 * i + torch.arange(s.N, dtype=torch.float32)).expand(s.M, -1))
+                 for i, s in enumerate(shapes))
+        # the max-over-ranks timing reduction bench.py uses
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        q.put((rank, ok, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_allgather_outputs_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res)
+    assert all(t == float(world) for _, _, t in res)
