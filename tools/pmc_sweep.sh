@@ -9,8 +9,8 @@ mkdir -p $OUT
 cd $REPO
 export TMPDIR=/tmp
 i=0
-GROUPS=${PMC_GROUPS:-"SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA|SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY|SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM SQ_INSTS_SALU GRBM_GUI_ACTIVE|FETCH_SIZE|TCC_HIT_sum TCC_MISS_sum|WRITE_SIZE TA_BUSY_avr TCP_TCC_READ_REQ_sum"}
-IFS='|' read -ra GRPS <<< "$GROUPS"
+PMC_LIST=${PMC_GROUPS:-"SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA|SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY|SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM SQ_INSTS_SALU GRBM_GUI_ACTIVE|FETCH_SIZE|TCC_HIT_sum TCC_MISS_sum|WRITE_SIZE TA_BUSY_avr TCP_TCC_READ_REQ_sum"}
+IFS='|' read -ra GRPS <<< "$PMC_LIST"
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 tools/kbench.py "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; }
