@@ -48,7 +48,7 @@ struct TileGeom {
   int bm, bn, bkb, threads;
 };
 
-enum class Kind { V0, V2 };
+enum class Kind { V0, V2, V3 };
 
 struct Variant {
   const char* name;
@@ -71,6 +71,10 @@ void launch_v2(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(gg_v2_kernel, dim3(grid), dim3(512), 0, s, a);
 }
 
+void launch_v3(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(gg_v3_kernel, dim3(grid), dim3(512), 0, s, a);
+}
+
 template <class C16, class C8, class C4>
 Variant make_v0(const char* name) {
   Variant v;
@@ -85,6 +89,20 @@ Variant make_v0(const char* name) {
   v.k_stage_bytes = 0;
   v.tail_bm = 0;
   v.launch = &launch_v0<C16, C8, C4>;
+  return v;
+}
+
+Variant make_v3(const char* name) {
+  Variant v;
+  v.name = name;
+  v.kind = Kind::V3;
+  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 64, 512};
+  v.threads = 512;
+  v.lds_bytes = V3Cfg<256>::LDS_BYTES;
+  v.chunk = 32;
+  v.k_stage_bytes = 0;
+  v.tail_bm = 128;
+  v.launch = &launch_v3;
   return v;
 }
 
@@ -112,6 +130,7 @@ const std::vector<Variant>& variants() {
       make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
       make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
       make_v2("v2_256x256_w8_dma"),
+      make_v3("v3_256x256_w8_dma_ring4"),
   };
   return v;
 }
@@ -244,7 +263,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     std::vector<std::pair<int, int>> mt;  // (m0, cls)
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
-      if (v.kind == Kind::V2 && v.tail_bm && rem <= v.tail_bm) {
+      if (v.kind != Kind::V0 && v.tail_bm && rem <= v.tail_bm) {
         mt.push_back({m0, 1});
         m0 += v.tail_bm;
       } else {

@@ -584,4 +584,241 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   }
 }
 
+
+// ============================================================================================
+// v3: as v2 (8 waves 2M x 4N, BN = 256, height classes 256 / 128, LDS-DMA, swapped MFMA operands,
+// LDS-staged epilogue) but K is staged 64 BYTES at a time through a 4-deep LDS ring with a
+// prefetch distance of 3 stages: the DMAs of stages s+1 and s+2 stay in flight across the barrier
+// of stage s (counted `s_waitcnt vmcnt(N)` + raw `s_barrier`, never vmcnt(0) in the loop).
+//   LDS rows are 64 B (4 x 16-B chunks); chunk c of row r sits at c ^ T[(r >> 2) & 3],
+//   T = {0, 2, 3, 1} — conflict-free for the 16-row ds_read_b128 (int8 / fp16) and ds_read_b64
+//   (int4) fragment reads (exhaustive check over the gfx950 lane groups).
+// Ring safety: stage s+3 is written into the buffer stage s-1 was read from; the barrier of
+// iteration s follows every wave's compute(s-1) (its ds_reads are consumed by MFMAs before it).
+// ============================================================================================
+template <int BM_>
+struct V3Cfg {
+  static constexpr int BM = BM_, BN = 256, NT = 512, BKB = 64, NBUF = 4, DIST = 3;
+  static constexpr int WM = 2, WN = 4;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB, STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int GA = BM / 128, GB = BN / 128;  // LDS-DMA wave-instructions per wave per stage
+  static constexpr int DMA_PER_STAGE = GA + GB;
+  static constexpr int EPI_BYTES = WM * WN * WTM * WTN * 2;
+  static constexpr int RING_BYTES = NBUF * STAGE_BYTES;
+  static constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+  static_assert(WTN == 64, "epilogue assumes 128-B staged rows");
+  static_assert(GA >= 1 && GB >= 1, "each wave issues at least one DMA per operand");
+};
+
+__device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }  // T = {0,2,3,1}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS barrier that lets LDS-DMA stay in flight: drain this wave's LDS reads, barrier, and keep the
+// compiler from moving LDS accesses across it (the "memory" clobbers) — unlike __syncthreads(),
+// no vmcnt(0).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <class Cfg, int QT>
+__device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __restrict__ A,
+                                           const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
+                                           const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
+                                           uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB, DPS = Cfg::DMA_PER_STAGE;
+  typedef typename AccT<QT>::type acc_t;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N, kbytes = mt.kbytes;
+  const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
+  const int nst = (kbytes + Cfg::BKB - 1) / Cfg::BKB;
+
+  // per-lane DMA sources: one wave-instruction = 16 rows x 64 B; lane -> (row r0 + lane/4, slot lane%4)
+  const uint8_t* srcA[GA];
+  const uint8_t* srcB[GB];
+  int kcA[GA], kcB[GB];  // logical chunk byte offset of this lane (for the K tail)
+  {
+    const int rsub = lane >> 2, p = lane & 3;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int row = (wave * GA + j) * 16 + rsub;
+      kcA[j] = (p ^ swz64(row)) << 4;
+      srcA[j] = A + (int64_t)min(m0 + row, M - 1) * lda + kcA[j];
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = (wave * GB + j) * 16 + rsub;
+      kcB[j] = (p ^ swz64(row)) << 4;
+      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + kcB[j];
+    }
+  }
+  const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
+  auto issue = [&](int s) {
+    uint8_t* As = lds + (s % Cfg::NBUF) * Cfg::STAGE_BYTES;
+    uint8_t* Bs = As + Cfg::A_BYTES;
+    const int kb = s * Cfg::BKB;
+    if (kb + Cfg::BKB <= kbytes) {
+#pragma unroll
+      for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
+    } else {  // K tail: lanes past K load 16 zero bytes
+#pragma unroll
+      for (int j = 0; j < GA; ++j) glds16(kb + kcA[j] < kbytes ? srcA[j] + kb : zero, As + (wave * GA + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) glds16(kb + kcB[j] < kbytes ? srcB[j] + kb : zero, Bs + (wave * GB + j) * 1024);
+    }
+  };
+
+  acc_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+
+  const int sw = swz64(r16);
+  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 64u;
+  const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 64u;
+  auto compute = [&](int s) {
+    const uint8_t* As = lds + (s % Cfg::NBUF) * Cfg::STAGE_BYTES + a_row;
+    const uint8_t* Bs = lds + (s % Cfg::NBUF) * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
+    if constexpr (QT == QT_I4) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {  // 2 x 32 bytes (= 64 int4) per 64-B stage
+        const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ sw) << 4) + (uint32_t)((g & 1) * 8);
+        v4i a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 1024 + off));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 1024 + off));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const uint32_t off = (uint32_t)((g ^ sw) << 4);
+      if constexpr (QT == QT_I8) {
+        v4i a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v4i*>(As + i * 1024 + off);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v4i*>(Bs + j * 1024 + off);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+      } else {
+        v8h a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v8h*>(As + i * 1024 + off);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v8h*>(Bs + j * 1024 + off);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- mainloop: 4-deep ring, 3 stages in flight ----
+#pragma unroll
+  for (int p = 0; p < Cfg::DIST; ++p)
+    if (p < nst) issue(p);
+  for (int s = 0; s < nst; ++s) {
+    const int later = min(Cfg::DIST - 1, nst - 1 - s);  // stages issued after s so far
+    if (later >= 2) wait_vmcnt<2 * DPS>();
+    else if (later == 1) wait_vmcnt<DPS>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // stage s landed for every wave; every wave is done with buffer (s-1)%4
+    if (s + Cfg::DIST < nst) issue(s + Cfg::DIST);
+    compute(s);
+  }
+  wait_vmcnt<0>();
+  lds_barrier();  // ring -> epilogue staging
+
+  // ---- epilogue (same as v2): per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
+  uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
+  const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
+  _Float16 sa[FM];
+  _Float16 sb[FN][4];
+  if constexpr (QT != QT_F16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) sa[i] = SA[min(mrow0 + i * 16 + r16, M - 1)];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = min(ncol0 + j * 16 + 4 * g, N - 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sb[j][r] = SB[n + r];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = i * 16 + r16;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      _Float16 h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (QT == QT_F16) {
+          h[r] = (_Float16)acc[i][j][r];
+        } else {
+          constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
+          const _Float16 s16 = sa[i] * sb[j][r];
+          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
+          asm volatile("" : "+v"(prod));
+          h[r] = (_Float16)(0.0f + prod);
+        }
+      }
+      const int q = 2 * j + (g >> 1);
+      uint2 pk;
+      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
+      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
+      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
+    }
+  }
+#pragma unroll 4
+  for (int it = 0; it < Cfg::WTM / 8; ++it) {
+    const int row = it * 8 + (lane >> 3), q = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
+    const int m = mrow0 + row, n = ncol0 + q * 8;
+    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+  }
+}
+
+__global__ __launch_bounds__(512, 2) void gg_v3_kernel(GGArgs args) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[V3Cfg<256>::LDS_BYTES];
+  const TileDesc td = args.tiles[blockIdx.x];
+  if (td.prob < 0) return;
+  const GGMeta mt = args.meta[td.prob];
+  const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[td.prob]);
+  const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[td.prob]);
+  const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
+  const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
+  _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
+  const bool tall = td.cls == 0;
+  if (mt.qtype == QT_I8) {
+    if (tall) gg_tile_v3<V3Cfg<256>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<V3Cfg<128>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if (mt.qtype == QT_I4) {
+    if (tall) gg_tile_v3<V3Cfg<256>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<V3Cfg<128>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else {
+    if (tall) gg_tile_v3<V3Cfg<256>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<V3Cfg<128>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  }
+}
+
 }  // namespace mxmoe

@@ -37,7 +37,7 @@ def _gpu():
     nat.lib()
 
 
-NV = 4  # compiled variants (tests/test_abi checks the count)
+NV = 5  # compiled variants (tests/test_abi checks the count)
 
 
 def _kbytes_ok(variant, K, q):
@@ -123,7 +123,7 @@ def test_unsupported_qtype_raises():
         group_gemm([p])
 
 
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", [0, 3, 4])
 def test_graph_capture_replay(variant):
     hps = [HostProblem(150, 256, 512, W8A8, seed=31, device=DEV), HostProblem(90, 128, 256, W4A4, seed=32, device=DEV)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)
