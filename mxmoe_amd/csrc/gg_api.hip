@@ -67,8 +67,9 @@ void launch_v0(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((gg_fused_kernel<C16, C8, C4>), dim3(grid), dim3(C16::kThreads), 0, s, a);
 }
 
+template <int ABL>
 void launch_v2(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(gg_v2_kernel, dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(gg_v2_kernel<ABL>, dim3(grid), dim3(512), 0, s, a);
 }
 
 void launch_v3(const GGArgs& a, int grid, hipStream_t s) {
@@ -106,6 +107,7 @@ Variant make_v3(const char* name) {
   return v;
 }
 
+template <int ABL = 0>
 Variant make_v2(const char* name) {
   Variant v;
   v.name = name;
@@ -116,7 +118,7 @@ Variant make_v2(const char* name) {
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
   v.k_stage_bytes = 0;  // K tails handled in-kernel (last stage)
   v.tail_bm = 128;
-  v.launch = &launch_v2;
+  v.launch = &launch_v2<ABL>;
   return v;
 }
 
@@ -131,6 +133,9 @@ const std::vector<Variant>& variants() {
       make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
       make_v2("v2_256x256_w8_dma"),
       make_v3("v3_256x256_w8_dma_ring4"),
+      // timing ablations of v2 (WRONG RESULTS by design; tools/kbench.py A/B only)
+      make_v2<ABL_NO_DMA>("abl_v2_nodma"),
+      make_v2<ABL_NO_EPI>("abl_v2_noepi"),
   };
   return v;
 }

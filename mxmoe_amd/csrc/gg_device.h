@@ -381,7 +381,11 @@ __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
 
-template <class Cfg, int QT>
+// ABL (timing ablations only, results are garbage): 1 = no mainloop DMA (stage 0 reused),
+// 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores.
+enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4 };
+
+template <class Cfg, int QT, int ABL = 0>
 __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
                                            const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
@@ -415,6 +419,9 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
   }
   auto issue = [&](int s, int buf) {
+    if constexpr ((ABL & ABL_NO_DMA) != 0) {
+      if (s > 0) return;
+    }
     uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
     uint8_t* Bs = As + Cfg::A_BYTES;
     const int kb = s * Cfg::BKB;
@@ -472,10 +479,23 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         const uint32_t off = (uint32_t)(((kc * 4 + g) ^ swz) << 4);
         if constexpr (QT == QT_I8) {
           v4i a[FM], b[FN];
+          if constexpr ((ABL & ABL_NO_LDS) != 0) {
 #pragma unroll
-          for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v4i*>(As + i * 2048 + off);
+            for (int i = 0; i < FM; ++i) {
+              a[i] = v4i{lane + i, kc, buf, 7};
+              asm volatile("" : "+v"(a[i]));
+            }
 #pragma unroll
-          for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v4i*>(Bs + j * 2048 + off);
+            for (int j = 0; j < FN; ++j) {
+              b[j] = v4i{lane - j, kc, 3, buf};
+              asm volatile("" : "+v"(b[j]));
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v4i*>(As + i * 2048 + off);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v4i*>(Bs + j * 2048 + off);
+          }
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -556,11 +576,16 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     const int row = it * 8 + (lane >> 3), q = lane & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
     const int m = mrow0 + row, n = ncol0 + q * 8;
-    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+    if constexpr ((ABL & ABL_NO_EPI) != 0) {
+      asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    } else {
+      if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+    }
   }
 }
 
 // v2 fused kernel: qtype x height-class dispatch, uniform per workgroup.
+template <int ABL>
 __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
   const TileDesc td = args.tiles[blockIdx.x];
@@ -573,14 +598,16 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
   const bool tall = td.cls == 0;
   if (mt.qtype == QT_I8) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if constexpr (ABL != 0) {
+    return;  // ablation builds time the int8 path only
   } else if (mt.qtype == QT_I4) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   }
 }
 
