@@ -132,6 +132,11 @@ def variant_count() -> int:
     return lib().mxmoe_gg_variant_count()
 
 
+def production_variants() -> list[int]:
+    """Compiled variants that compute correct results (``abl_*`` are timing ablations)."""
+    return [int(ln.split()[0]) for ln in list_variants() if not ln.split()[1].startswith("abl_")]
+
+
 def default_variant() -> int:
     return lib().mxmoe_gg_default_variant()
 

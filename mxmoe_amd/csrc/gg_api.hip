@@ -72,8 +72,9 @@ void launch_v2(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(gg_v2_kernel<ABL>, dim3(grid), dim3(512), 0, s, a);
 }
 
+template <int BN, int WN, int NBUF, int DIST>
 void launch_v3(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(gg_v3_kernel, dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((gg_v3_kernel<BN, WN, NBUF, DIST>), dim3(grid), dim3(V3Cfg<256, BN, WN>::NT), 0, s, a);
 }
 
 template <class C16, class C8, class C4>
@@ -93,17 +94,19 @@ Variant make_v0(const char* name) {
   return v;
 }
 
+template <int BN, int WN, int NBUF, int DIST>
 Variant make_v3(const char* name) {
+  typedef V3Cfg<256, BN, WN, NBUF, DIST> CT;
   Variant v;
   v.name = name;
   v.kind = Kind::V3;
-  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 64, 512};
-  v.threads = 512;
-  v.lds_bytes = V3Cfg<256>::LDS_BYTES;
-  v.chunk = 32;
+  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};
+  v.threads = CT::NT;
+  v.lds_bytes = CT::LDS_BYTES;
+  v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
   v.k_stage_bytes = 0;
   v.tail_bm = 128;
-  v.launch = &launch_v3;
+  v.launch = &launch_v3<BN, WN, NBUF, DIST>;
   return v;
 }
 
@@ -132,10 +135,11 @@ const std::vector<Variant>& variants() {
       make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
       make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
       make_v2("v2_256x256_w8_dma"),
-      make_v3("v3_256x256_w8_dma_ring4"),
+      make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
       // timing ablations of v2 (WRONG RESULTS by design; tools/kbench.py A/B only)
       make_v2<ABL_NO_DMA>("abl_v2_nodma"),
       make_v2<ABL_NO_EPI>("abl_v2_noepi"),
+      make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
   };
   return v;
 }

@@ -623,20 +623,22 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
 // Ring safety: stage s+3 is written into the buffer stage s-1 was read from; the barrier of
 // iteration s follows every wave's compute(s-1) (its ds_reads are consumed by MFMAs before it).
 // ============================================================================================
-template <int BM_>
+template <int BM_, int BN_ = 256, int WN_ = 4, int NBUF_ = 4, int DIST_ = 3>
 struct V3Cfg {
-  static constexpr int BM = BM_, BN = 256, NT = 512, BKB = 64, NBUF = 4, DIST = 3;
-  static constexpr int WM = 2, WN = 4;
+  static constexpr int BM = BM_, BN = BN_, BKB = 64, NBUF = NBUF_, DIST = DIST_;
+  static constexpr int WM = 2, WN = WN_, NT = WM * WN * 64, NWAVES = WM * WN;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
   static constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB, STAGE_BYTES = A_BYTES + B_BYTES;
-  static constexpr int GA = BM / 128, GB = BN / 128;  // LDS-DMA wave-instructions per wave per stage
+  // LDS-DMA wave-instructions per wave per stage (one covers 16 rows x 64 B)
+  static constexpr int GA = BM / (16 * NWAVES), GB = BN / (16 * NWAVES);
   static constexpr int DMA_PER_STAGE = GA + GB;
   static constexpr int EPI_BYTES = WM * WN * WTM * WTN * 2;
   static constexpr int RING_BYTES = NBUF * STAGE_BYTES;
   static constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
   static_assert(WTN == 64, "epilogue assumes 128-B staged rows");
   static_assert(GA >= 1 && GB >= 1, "each wave issues at least one DMA per operand");
+  static_assert(DIST < NBUF && DIST <= 3, "ring: stage s+DIST reuses the buffer of stage s-1 at most");
 };
 
 __device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }  // T = {0,2,3,1}
@@ -825,8 +827,11 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
   }
 }
 
-__global__ __launch_bounds__(512, 2) void gg_v3_kernel(GGArgs args) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[V3Cfg<256>::LDS_BYTES];
+template <int BN, int WN, int NBUF, int DIST>
+__global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2 waves/SIMD: <= 256 VGPRs
+  typedef V3Cfg<256, BN, WN, NBUF, DIST> CT;
+  typedef V3Cfg<128, BN, WN, NBUF, DIST> CS;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[CT::LDS_BYTES];
   const TileDesc td = args.tiles[blockIdx.x];
   if (td.prob < 0) return;
   const GGMeta mt = args.meta[td.prob];
@@ -837,15 +842,16 @@ __global__ __launch_bounds__(512, 2) void gg_v3_kernel(GGArgs args) {
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
   const bool tall = td.cls == 0;
   if (mt.qtype == QT_I8) {
-    if (tall) gg_tile_v3<V3Cfg<256>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v3<V3Cfg<128>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v3<CT, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<CS, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else if (mt.qtype == QT_I4) {
-    if (tall) gg_tile_v3<V3Cfg<256>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v3<V3Cfg<128>, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v3<CT, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<CS, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else {
-    if (tall) gg_tile_v3<V3Cfg<256>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v3<V3Cfg<128>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v3<CT, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<CS, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   }
 }
+
 
 }  // namespace mxmoe

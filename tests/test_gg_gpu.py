@@ -37,14 +37,14 @@ def _gpu():
     nat.lib()
 
 
-NV = 5  # compiled variants (tests/test_abi checks the count)
+PROD = nat.production_variants()  # every correct compiled variant (abl_* excluded)
 
 
 def _kbytes_ok(variant, K, q):
     return True  # every variant handles K tails (multiples of 16 bytes)
 
 
-@pytest.mark.parametrize("variant", range(NV))
+@pytest.mark.parametrize("variant", PROD)
 @pytest.mark.parametrize("q", [FP16, W8A8, W4A4], ids=["fp16", "w8a8", "w4a4"])
 def test_single_qtype_edge_shapes(q, variant):
     shapes = [(1, 128, 256), (17, 256, 128), (130, 128, 384), (257, 136, 512), (64, 8, 1024), (300, 520, 512),
@@ -56,7 +56,7 @@ def test_single_qtype_edge_shapes(q, variant):
     _check(hps)
 
 
-@pytest.mark.parametrize("variant", range(NV))
+@pytest.mark.parametrize("variant", PROD)
 def test_mixed_fused_launch(variant):
     specs = [(300, 256, 256, W8A8), (0, 256, 256, W4A4), (129, 384, 512, W4A4), (77, 128, 192, FP16),
              (513, 256, 128, W8A8), (5, 128, 64, W4A4), (256, 256, 256, FP16), (384, 512, 1024, W8A8)]
@@ -72,7 +72,7 @@ def test_mixed_fused_launch(variant):
     _check(hps)
 
 
-@pytest.mark.parametrize("variant", range(NV))
+@pytest.mark.parametrize("variant", PROD)
 @pytest.mark.parametrize("q", [W8A8, W4A4, FP16], ids=["w8a8", "w4a4", "fp16"])
 def test_k_tail_inside_stage(q, variant):
     # K bytes not a multiple of the 128-B stage: the tail must not change the sum
@@ -84,7 +84,7 @@ def test_k_tail_inside_stage(q, variant):
     _check(hps)
 
 
-@pytest.mark.parametrize("variant", range(NV))
+@pytest.mark.parametrize("variant", PROD)
 def test_strided_c_nslices(variant):
     # two N-slices of one logical problem written into one C buffer with ldc = N_total
     M, N, K = 200, 512, 256
@@ -123,7 +123,7 @@ def test_unsupported_qtype_raises():
         group_gemm([p])
 
 
-@pytest.mark.parametrize("variant", [0, 3, 4])
+@pytest.mark.parametrize("variant", [v for v in PROD if v >= 3] + [0])
 def test_graph_capture_replay(variant):
     hps = [HostProblem(150, 256, 512, W8A8, seed=31, device=DEV), HostProblem(90, 128, 256, W4A4, seed=32, device=DEV)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)

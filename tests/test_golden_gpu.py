@@ -62,7 +62,7 @@ def _verify(probs, exp):
 
 
 @pytest.mark.parametrize("name", ["gg_w8a8_small.npz", "gg_w4a4_small.npz", "gg_fp16_small.npz", "gg_mixed_small.npz"])
-@pytest.mark.parametrize("variant", range(5))
+@pytest.mark.parametrize("variant", nat.production_variants())
 def test_golden_vectors(name, variant):
     probs, exp = _load(name)
     group_gemm(probs, variant=variant)
@@ -101,7 +101,7 @@ def _sample_check(inputs, n_rows=48, n_cols=48, seed=0):
             assert_f16_close(out, ref, p.K)
 
 
-@pytest.mark.parametrize("variant", [0, 3, 4])
+@pytest.mark.parametrize("variant", [v for v in nat.production_variants() if v >= 3] + [0])
 @pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed"])
 def test_full_size_layer11_sampled_parity(cfg, variant):
     from mxmoe_amd.harness import build_layer_inputs
