@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="fp16", choices=list(CONFIGS))
-    ap.add_argument("--variant", type=int, default=-1, help="-1 = default variant for the config")
+    ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extras", default="w8a8,mixed", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
@@ -134,11 +134,12 @@ def main():
     from mxmoe_amd.harness import build_layer_inputs, time_launches
 
     def run_config(cfg: str, steps: int, warmup: int, timed_region: bool):
-        variant = args.variant if args.variant >= 0 else default_variant(cfg)
+        variant = args.variant if args.variant >= 0 else None
         shapes = layer_shapes(cfg, world, rank)
         inp = {gg: build_layer_inputs(shapes[gg], device=dev, seed=42 + 1000 * rank + (gg == "down"))
                for gg in ("gate_up", "down")}
         ggs = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
+        variant = ggs["gate_up"].variant  # concrete (AUTO resolved by the library)
         flops = {gg: inp[gg].flops for gg in inp}
         stream = torch.cuda.current_stream(dev)
 
@@ -239,7 +240,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4),
                          "traffic": pmc.get("hbm_bytes_per_step") if isinstance(pmc, dict) else None,
-                         "kernel": ("mxmoe::gg_v2_kernel" if main_res["variant"] == 3 else "mxmoe::gg_fused_kernel")
+                         "kernel": kernel_symbol(nat.list_variants()[main_res["variant"]].split()[1])
                          + " (gate_up + down launches; achieved = sum FLOPs / sum mean launch time)",
                          "launch_ms": {"gate_up": round(t_gu, 4), "down": round(t_dn, 4)}},
             "cpu_baseline": cpu,
@@ -250,10 +251,10 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def default_variant(cfg: str) -> int:
-    from mxmoe_amd import _native as nat
-
-    return nat.default_variant()
+def kernel_symbol(variant_name: str) -> str:
+    """Kernel template a variant launches (the name rocprofv3 reports)."""
+    return {"v0": "mxmoe::gg_fused_kernel", "v2": "mxmoe::gg_v2_kernel", "v3": "mxmoe::gg_v3_kernel"}.get(
+        variant_name.split("_")[0], variant_name)
 
 
 if __name__ == "__main__":

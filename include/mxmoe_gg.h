@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MXMOE_GG_ABI_VERSION 1
+#define MXMOE_GG_ABI_VERSION 2
 
 enum {
   MXMOE_GG_OK = 0,
@@ -82,6 +82,9 @@ typedef struct mxmoe_gg_plan_info {
   int32_t grid;
   int32_t block;
   int32_t lds_bytes;
+  int32_t qtype_mask;      /* bit q set if a planned problem has quant type q (0 fp16, 1 w8a8, 2 w4a4);
+                            * selects the kernel specialisation at launch */
+  int32_t reserved_;
   int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */
   void* workspace;         /* device workspace the plan was written to */
 } mxmoe_gg_plan_info;
@@ -94,7 +97,7 @@ const char* mxmoe_gg_last_error(void);
 /* Number of compiled kernel variants. */
 int mxmoe_gg_variant_count(void);
 
-/* The variant used when the caller has no preference (and by groupgemm_mxmoe). */
+/* The variant AUTO resolves to for fp16 / w8a8-only problem sets. */
 int mxmoe_gg_default_variant(void);
 
 /* Writes a newline-separated description of every compiled variant into buf (truncated,
@@ -107,6 +110,10 @@ int mxmoe_gg_list_variants(char* buf, size_t n);
  * writes BM, BN, K-bytes-per-stage and threads per workgroup. */
 int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int32_t* bn, int32_t* bk_bytes,
                           int32_t* threads);
+
+/* Pass as `variant` to mxmoe_gg_workspace_size / _plan / _run: the library picks the variant
+ * from the quant types present (the plan info records the concrete one). groupgemm_mxmoe uses it. */
+#define MXMOE_GG_VARIANT_AUTO (-1)
 
 /* Device workspace bytes the plan of these problems needs with this variant
  * (plan table + pointer arrays + tile table). Validates the problems like mxmoe_gg_plan. */

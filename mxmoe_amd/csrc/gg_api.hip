@@ -59,22 +59,47 @@ struct Variant {
   int chunk;           // tiles per XCD chunk (workgroups that run together on one XCD)
   int k_stage_bytes;   // K bytes per row must be a multiple of this (0 = any multiple of 16)
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
-  void (*launch)(const GGArgs&, int grid, hipStream_t);
+  void (*launch)(const GGArgs&, int grid, int qmask, hipStream_t);  // qmask: 1 << QType present
 };
 
 template <class C16, class C8, class C4>
-void launch_v0(const GGArgs& a, int grid, hipStream_t s) {
+void launch_v0(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   hipLaunchKernelGGL((gg_fused_kernel<C16, C8, C4>), dim3(grid), dim3(C16::kThreads), 0, s, a);
 }
 
+template <int ABL, int QM>
+void launch_v2_q(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gg_v2_kernel<ABL, QM>), dim3(grid), dim3(512), 0, s, a);
+}
 template <int ABL>
-void launch_v2(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(gg_v2_kernel<ABL>, dim3(grid), dim3(512), 0, s, a);
+void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  if constexpr (ABL != 0) {
+    launch_v2_q<ABL, 7>(a, grid, s);
+  } else {
+    switch (qmask & 7) {
+      case 1: launch_v2_q<0, 1>(a, grid, s); break;
+      case 2: launch_v2_q<0, 2>(a, grid, s); break;
+      case 4: launch_v2_q<0, 4>(a, grid, s); break;
+      case 6: launch_v2_q<0, 6>(a, grid, s); break;
+      default: launch_v2_q<0, 7>(a, grid, s); break;
+    }
+  }
 }
 
+// v3 is specialised on the set of quant types the plan contains (mask 1 << QType)
+template <int BN, int WN, int NBUF, int DIST, int QM>
+void launch_v3_q(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gg_v3_kernel<BN, WN, NBUF, DIST, QM>), dim3(grid), dim3(V3Cfg<256, BN, WN>::NT), 0, s, a);
+}
 template <int BN, int WN, int NBUF, int DIST>
-void launch_v3(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gg_v3_kernel<BN, WN, NBUF, DIST>), dim3(grid), dim3(V3Cfg<256, BN, WN>::NT), 0, s, a);
+void launch_v3(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  switch (qmask & 7) {
+    case 1: launch_v3_q<BN, WN, NBUF, DIST, 1>(a, grid, s); break;
+    case 2: launch_v3_q<BN, WN, NBUF, DIST, 2>(a, grid, s); break;
+    case 4: launch_v3_q<BN, WN, NBUF, DIST, 4>(a, grid, s); break;
+    case 6: launch_v3_q<BN, WN, NBUF, DIST, 6>(a, grid, s); break;
+    default: launch_v3_q<BN, WN, NBUF, DIST, 7>(a, grid, s); break;
+  }
 }
 
 template <class C16, class C8, class C4>
@@ -144,7 +169,8 @@ const std::vector<Variant>& variants() {
   return v;
 }
 
-constexpr int kDefaultVariant = 3;  // v2 (fastest on every qwen2_moe layer-11 config)
+constexpr int kDefaultVariant = 3;  // v2 256x256 8 waves: fastest fp16 / w8a8 (qwen2_moe layer 11)
+constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";  // fastest once w4a4 is present
 
 int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
   if (a_bits == 16 && w_bits == 16) {
@@ -312,6 +338,25 @@ int check_variant(int variant) {
   return MXMOE_GG_OK;
 }
 
+// MXMOE_GG_VARIANT_AUTO -> concrete variant from the quant types present (profiles/r01 kbench):
+// any w4a4 problem -> the 256x128 / 2-workgroups-per-CU variant, otherwise the 256x256 one.
+int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
+  if (variant != MXMOE_GG_VARIANT_AUTO) {
+    *out = variant;
+    return check_variant(variant);
+  }
+  bool int4 = false;
+  for (const HostProblem& p : hp) {
+    int qt;
+    if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) == MXMOE_GG_OK && qt == QT_I4) int4 = true;
+  }
+  *out = kDefaultVariant;
+  if (int4)
+    for (size_t i = 0; i < variants().size(); ++i)
+      if (!strcmp(variants()[i].name, kInt4Variant)) *out = (int)i;
+  return MXMOE_GG_OK;
+}
+
 std::vector<HostProblem> to_host(const mxmoe_gg_problem* problems, int problem_count) {
   std::vector<HostProblem> hp(problem_count);
   for (int i = 0; i < problem_count; ++i) {
@@ -342,6 +387,9 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
   info->grid = (int)plan.tiles.size();
   info->block = v.threads;
   info->lds_bytes = v.lds_bytes;
+  info->qtype_mask = 0;
+  for (const GGMeta& m : plan.meta) info->qtype_mask |= 1 << m.qtype;
+  info->reserved_ = 0;
   info->workspace_bytes = (int64_t)l.total;
   info->workspace = ws;
 }
@@ -403,10 +451,11 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
 int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count, int variant, size_t* bytes) {
   if (problem_count < 0 || (problem_count > 0 && !problems) || !bytes)
     return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_workspace_size");
-  int st = check_variant(variant);
+  const std::vector<HostProblem> hp = to_host(problems, problem_count);
+  int st = resolve_variant(variant, hp, &variant);
   if (st) return st;
   Plan plan;
-  st = plan_host(to_host(problems, problem_count), variant, false, &plan);
+  st = plan_host(hp, variant, false, &plan);
   if (st) return st;
   *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size()).total;
   return MXMOE_GG_OK;
@@ -416,9 +465,9 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
                   size_t workspace_bytes, void* stream, mxmoe_gg_plan_info* info) {
   if (problem_count < 0 || (problem_count > 0 && !problems) || !info)
     return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_plan");
-  int st = check_variant(variant);
-  if (st) return st;
   const std::vector<HostProblem> hp = to_host(problems, problem_count);
+  int st = resolve_variant(variant, hp, &variant);
+  if (st) return st;
   Plan plan;
   st = plan_host(hp, variant, true, &plan);
   if (st) return st;
@@ -458,7 +507,7 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   a.ptr_C = reinterpret_cast<void* const*>(ws + l.meta + 4 * l.ptr);
   a.P = P;
   a.n_slots = info->grid;
-  variants()[info->variant].launch(a, info->grid, (hipStream_t)stream);
+  variants()[info->variant].launch(a, info->grid, info->qtype_mask, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return MXMOE_GG_OK;
 }
@@ -491,8 +540,11 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
     hp[i] = HostProblem{nullptr, nullptr, nullptr, nullptr, nullptr, (int)h_problem_sizes[i].x,
                         (int)h_problem_sizes[i].y, (int)h_problem_sizes[i].z, h_qbits_list[i].a_bits,
                         h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0};
+  int variant;
+  int st = resolve_variant(MXMOE_GG_VARIANT_AUTO, hp, &variant);
+  if (st) return st;
   Plan plan;
-  int st = plan_host(hp, kDefaultVariant, false, &plan);
+  st = plan_host(hp, variant, false, &plan);
   if (st) return st;
   if (plan.total_tiles == 0) return MXMOE_GG_OK;
   // gather the caller's device pointer arrays through the host (same sync cost class as the
@@ -519,7 +571,7 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
   }
   HIP_TRY(hipMemcpy(ws, img.data(), l.total, hipMemcpyHostToDevice));
   mxmoe_gg_plan_info info;
-  fill_info(plan, kDefaultVariant, l, ws, &info);
+  fill_info(plan, variant, l, ws, &info);
   return mxmoe_gg_launch(&info, nullptr);
 }
 

@@ -585,7 +585,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 }
 
 // v2 fused kernel: qtype x height-class dispatch, uniform per workgroup.
-template <int ABL>
+template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
 __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
   const TileDesc td = args.tiles[blockIdx.x];
@@ -597,15 +597,15 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
   const bool tall = td.cls == 0;
-  if (mt.qtype == QT_I8) {
+  if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     if (tall) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else if constexpr (ABL != 0) {
     return;  // ablation builds time the int8 path only
-  } else if (mt.qtype == QT_I4) {
+  } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
     if (tall) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  } else {
+  } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (tall) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   }
@@ -636,7 +636,7 @@ struct V3Cfg {
   static constexpr int EPI_BYTES = WM * WN * WTM * WTN * 2;
   static constexpr int RING_BYTES = NBUF * STAGE_BYTES;
   static constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
-  static_assert(WTN == 64, "epilogue assumes 128-B staged rows");
+  static_assert(WTN == 64 || WTN == 128, "epilogue stages 128-B or 256-B rows");
   static_assert(GA >= 1 && GB >= 1, "each wave issues at least one DMA per operand");
   static_assert(DIST < NBUF && DIST <= 3, "ring: stage s+DIST reuses the buffer of stage s-1 at most");
 };
@@ -655,6 +655,67 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// Epilogue shared by v3 / v4: dequant (int paths) + fp16 rounding, per-wave LDS staging of the
+// WTM x WTN fp16 sub-tile in XOR-swizzled 16-B chunks, then 16-B row stores (coalesced along N).
+// Needs WTM * WTN * 2 bytes of LDS per wave at `lds` (the drained ring).
+template <class Cfg, int QT>
+__device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>::type (&acc)[Cfg::FM][Cfg::FN],
+                                            const _Float16* __restrict__ SA, const _Float16* __restrict__ SB,
+                                            _Float16* __restrict__ C, int m0, int n0, uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N;
+  constexpr int RB = Cfg::WTN * 2, CPR = RB / 16;  // staged row bytes, 16-B chunks per row
+  uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
+  const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
+  // column scales: one 8-B load per 4 columns (N % 8 == 0 keeps the clamped address 8-B
+  // aligned); the row scale is loaded per fragment row -> 2*FN + 1 live registers, not 5*FN
+  uint2 sbw[FN];
+  if constexpr (QT != QT_F16) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(SB + min(ncol0 + j * 16 + 4 * g, N - 4));
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = i * 16 + r16;
+    _Float16 sai = 0;
+    if constexpr (QT != QT_F16) sai = SA[min(mrow0 + ml, M - 1)];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      _Float16 h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (QT == QT_F16) {
+          h[r] = (_Float16)acc[i][j][r];
+        } else {
+          constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
+          const uint32_t w = (r < 2) ? sbw[j].x : sbw[j].y;
+          const _Float16 s16 = sai * __builtin_bit_cast(_Float16, (uint16_t)(w >> (16 * (r & 1))));
+          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
+          asm volatile("" : "+v"(prod));
+          h[r] = (_Float16)(0.0f + prod);
+        }
+      }
+      const int q = 2 * j + (g >> 1);
+      uint2 pk;
+      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
+      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
+      *reinterpret_cast<uint2*>(reg + ml * RB + ((q ^ (ml & (CPR - 1))) << 4) + (g & 1) * 8) = pk;
+    }
+  }
+  constexpr int RPI = 64 / CPR;  // staged rows per wave-instruction
+#pragma unroll 4
+  for (int it = 0; it < Cfg::WTM / RPI; ++it) {
+    const int row = it * RPI + lane / CPR, q = lane % CPR;
+    const uint4 v = *reinterpret_cast<const uint4*>(reg + row * RB + ((q ^ (row & (CPR - 1))) << 4));
+    const int m = mrow0 + row, n = ncol0 + q * 8;
+    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+  }
 }
 
 template <class Cfg, int QT>
@@ -725,15 +786,15 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
       for (int st = 0; st < 2; ++st) {  // 2 x 32 bytes (= 64 int4) per 64-B stage
         const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ sw) << 4) + (uint32_t)((g & 1) * 8);
-        v4i a[FM], b[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 1024 + off));
+        v4i b[FN];  // B widened once, A per fragment row: 4 live widened registers instead of 4*FM
 #pragma unroll
         for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 1024 + off));
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) {
+          const v4i a = widen_i4(*reinterpret_cast<const v2i*>(As + i * 1024 + off));
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a, acc[i][j], 0, 0, 0);
+        }
       }
     } else {
       const uint32_t off = (uint32_t)((g ^ sw) << 4);
@@ -778,56 +839,12 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
   wait_vmcnt<0>();
   lds_barrier();  // ring -> epilogue staging
 
-  // ---- epilogue (same as v2): per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
-  uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
-  const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
-  _Float16 sa[FM];
-  _Float16 sb[FN][4];
-  if constexpr (QT != QT_F16) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i) sa[i] = SA[min(mrow0 + i * 16 + r16, M - 1)];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = min(ncol0 + j * 16 + 4 * g, N - 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sb[j][r] = SB[n + r];
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int ml = i * 16 + r16;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      _Float16 h[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (QT == QT_F16) {
-          h[r] = (_Float16)acc[i][j][r];
-        } else {
-          constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
-          const _Float16 s16 = sa[i] * sb[j][r];
-          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
-          asm volatile("" : "+v"(prod));
-          h[r] = (_Float16)(0.0f + prod);
-        }
-      }
-      const int q = 2 * j + (g >> 1);
-      uint2 pk;
-      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
-      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
-      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
-    }
-  }
-#pragma unroll 4
-  for (int it = 0; it < Cfg::WTM / 8; ++it) {
-    const int row = it * 8 + (lane >> 3), q = lane & 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
-    const int m = mrow0 + row, n = ncol0 + q * 8;
-    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
-  }
+  epilogue_v3<Cfg, QT>(mt, acc, SA, SB, C, m0, n0, lds);
 }
 
-template <int BN, int WN, int NBUF, int DIST>
+// QM = set of quant types compiled in (bit 1 << QType, chosen by the plan): a single-type launch
+// carries one tile body, not three
+template <int BN, int WN, int NBUF, int DIST, int QM>
 __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2 waves/SIMD: <= 256 VGPRs
   typedef V3Cfg<256, BN, WN, NBUF, DIST> CT;
   typedef V3Cfg<128, BN, WN, NBUF, DIST> CS;
@@ -841,17 +858,18 @@ __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2
   const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
   const bool tall = td.cls == 0;
-  if (mt.qtype == QT_I8) {
+  if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     if (tall) gg_tile_v3<CT, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v3<CS, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  } else if (mt.qtype == QT_I4) {
+  } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
     if (tall) gg_tile_v3<CT, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v3<CS, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  } else {
+  } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (tall) gg_tile_v3<CT, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v3<CS, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   }
 }
+
 
 
 }  // namespace mxmoe

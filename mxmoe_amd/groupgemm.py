@@ -113,7 +113,9 @@ class GroupGemm:
     def __init__(self, problems: Sequence[Problem], variant: Optional[int] = None,
                  device: Optional[torch.device] = None, stream: Optional[torch.cuda.Stream] = None):
         self.problems = list(problems)
-        self.variant = nat.default_variant() if variant is None else int(variant)
+        # None -> MXMOE_GG_VARIANT_AUTO (-1): the library picks by quant-type mix; after planning
+        # self.variant is the concrete variant
+        self.variant = nat.VARIANT_AUTO if variant is None else int(variant)
         if device is None:
             device = self.problems[0].C.device if self.problems else torch.device("cuda")
         self.device = device
@@ -128,6 +130,7 @@ class GroupGemm:
         self.info = nat.GGPlanInfo()
         nat.check(nat.lib().mxmoe_gg_plan(self._c_problems, P, self.variant, ctypes.c_void_p(self.workspace.data_ptr()),
                                           ws_bytes, ctypes.c_void_p(_stream_handle(stream)), ctypes.byref(self.info)))
+        self.variant = int(self.info.variant)
 
     @property
     def total_tiles(self) -> int:

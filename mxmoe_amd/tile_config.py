@@ -128,6 +128,8 @@ def mi355x_variants() -> list[dict]:
         for q in _VQ_RE.finditer(m.group(3)):
             bm, bn, bk, wm, wn, wk, st = map(int, q.groups()[1:])
             tiles[q.group(1)] = TileConfig(BM=bm, BN=bn, BK=bk, WM=wm, WN=wn, WK=wk, STAGE=st)
+        if m.group(2).startswith("abl_"):
+            continue  # timing ablations compute wrong results by design
         out.append({"id": int(m.group(1)), "name": m.group(2), "tiles": tiles})
     return out
 

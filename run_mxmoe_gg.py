@@ -114,7 +114,7 @@ def main(argv=None):
             tiles = parse_tile_config_json(args.tile_config, qcfg_list, layer)
             variants = [select_variant(tiles, nat.default_variant())]
         else:
-            variants = list(range(nat.variant_count()))
+            variants = nat.production_variants()
         names = nat.list_variants()
         parsed = load_workload(wl)[f"layer-{layer}"]
         for gg in ("gate_up", "down"):

@@ -41,7 +41,7 @@ def test_struct_layouts():
 
 
 def test_abi_version_and_variants():
-    assert nat.lib().mxmoe_gg_abi_version() == 1
+    assert nat.lib().mxmoe_gg_abi_version() == 2
     vs = nat.list_variants()
     assert len(vs) == nat.variant_count() >= 1
     assert "w8a8_g-1_sym=TileConfig(" in vs[0]
@@ -58,6 +58,28 @@ def test_workspace_size_grows_with_tiles():
     big = ws([_prob(M=8192, N=4096)])
     assert 0 < small < big
     assert ws([_prob(M=0)]) > 0  # empty problems plan to an empty tile table
+
+
+def test_struct_plan_info_layout():
+    assert ctypes.sizeof(nat.GGPlanInfo) == 8 * 4 + 8 + 8  # qtype_mask + reserved keep the int64 aligned
+
+
+def test_auto_variant_follows_quant_mix():
+    """MXMOE_GG_VARIANT_AUTO: int4 present -> the 256x128 variant, else the default (256x256)."""
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    int4_v = names.index("v3_256x128_w4_dma_ring3_2wg")
+
+    def ws(ps, v):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.workspace_size(arr, len(ps), v)
+
+    big = dict(M=4096, N=4096, K=1024)
+    w8 = [_prob(**big)]
+    mix = [_prob(**big), _prob(a_bits=4, w_bits=4, **big)]
+    assert ws(w8, nat.VARIANT_AUTO) == ws(w8, nat.default_variant())
+    assert ws(mix, nat.VARIANT_AUTO) == ws(mix, int4_v) != ws(mix, nat.default_variant())
+    # an empty int4 problem does not count
+    assert ws(w8 + [_prob(a_bits=4, w_bits=4, M=0)], nat.VARIANT_AUTO) == ws(w8 + [_prob(M=0)], nat.default_variant())
 
 
 def _plan(problems, ws_bytes=1 << 20):
