@@ -254,7 +254,7 @@ def main():
 def kernel_symbol(variant_name: str) -> str:
     """Kernel template a variant launches (the name rocprofv3 reports)."""
     return {"v0": "mxmoe::gg_fused_kernel", "v2": "mxmoe::gg_v2_kernel", "v3": "mxmoe::gg_v3_kernel"}.get(
-        variant_name.split("_")[0], variant_name)
+        variant_name[:2], variant_name)
 
 
 if __name__ == "__main__":

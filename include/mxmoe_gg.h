@@ -97,7 +97,7 @@ const char* mxmoe_gg_last_error(void);
 /* Number of compiled kernel variants. */
 int mxmoe_gg_variant_count(void);
 
-/* The variant AUTO resolves to for fp16 / w8a8-only problem sets. */
+/* The variant AUTO resolves to unless every non-empty problem is w4a4. */
 int mxmoe_gg_default_variant(void);
 
 /* Writes a newline-separated description of every compiled variant into buf (truncated,

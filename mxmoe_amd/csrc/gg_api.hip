@@ -73,15 +73,15 @@ void launch_v2_q(const GGArgs& a, int grid, hipStream_t s) {
 }
 template <int ABL>
 void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
-  if constexpr (ABL != 0) {
+  if constexpr ((ABL & 7) != 0) {
     launch_v2_q<ABL, 7>(a, grid, s);
   } else {
     switch (qmask & 7) {
-      case 1: launch_v2_q<0, 1>(a, grid, s); break;
-      case 2: launch_v2_q<0, 2>(a, grid, s); break;
-      case 4: launch_v2_q<0, 4>(a, grid, s); break;
-      case 6: launch_v2_q<0, 6>(a, grid, s); break;
-      default: launch_v2_q<0, 7>(a, grid, s); break;
+      case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
+      case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
+      case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
+      case 6: launch_v2_q<ABL, 6>(a, grid, s); break;
+      default: launch_v2_q<ABL, 7>(a, grid, s); break;
     }
   }
 }
@@ -165,12 +165,21 @@ const std::vector<Variant>& variants() {
       make_v2<ABL_NO_DMA>("abl_v2_nodma"),
       make_v2<ABL_NO_EPI>("abl_v2_noepi"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
+      make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
   };
   return v;
 }
 
-constexpr int kDefaultVariant = 3;  // v2 256x256 8 waves: fastest fp16 / w8a8 (qwen2_moe layer 11)
-constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";  // fastest once w4a4 is present
+// AUTO policy (profiles/r01/kbench_*.jsonl, qwen2_moe layer 11): the staggered 256x256 v2 is the
+// fastest whenever fp16 or w8a8 problems are present; int4-only sets run 256x128 tiles, 2 WG/CU.
+constexpr const char* kDefaultVariantName = "v2s_256x256_w8_dma_stagger";
+constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
+
+int variant_index(const char* name) {
+  for (size_t i = 0; i < variants().size(); ++i)
+    if (!strcmp(variants()[i].name, name)) return (int)i;
+  return 0;
+}
 
 int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
   if (a_bits == 16 && w_bits == 16) {
@@ -338,22 +347,18 @@ int check_variant(int variant) {
   return MXMOE_GG_OK;
 }
 
-// MXMOE_GG_VARIANT_AUTO -> concrete variant from the quant types present (profiles/r01 kbench):
-// any w4a4 problem -> the 256x128 / 2-workgroups-per-CU variant, otherwise the 256x256 one.
+// MXMOE_GG_VARIANT_AUTO -> concrete variant from the quant types present (policy above).
 int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   if (variant != MXMOE_GG_VARIANT_AUTO) {
     *out = variant;
     return check_variant(variant);
   }
-  bool int4 = false;
+  int mask = 0;
   for (const HostProblem& p : hp) {
     int qt;
-    if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) == MXMOE_GG_OK && qt == QT_I4) int4 = true;
+    if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) == MXMOE_GG_OK) mask |= 1 << qt;
   }
-  *out = kDefaultVariant;
-  if (int4)
-    for (size_t i = 0; i < variants().size(); ++i)
-      if (!strcmp(variants()[i].name, kInt4Variant)) *out = (int)i;
+  *out = variant_index(mask == (1 << QT_I4) ? kInt4Variant : kDefaultVariantName);
   return MXMOE_GG_OK;
 }
 
@@ -404,7 +409,7 @@ const char* mxmoe_gg_last_error(void) { return g_last_error.c_str(); }
 
 int mxmoe_gg_variant_count(void) { return (int)variants().size(); }
 
-int mxmoe_gg_default_variant(void) { return kDefaultVariant; }
+int mxmoe_gg_default_variant(void) { return variant_index(kDefaultVariantName); }
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
   static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym"};

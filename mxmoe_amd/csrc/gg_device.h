@@ -381,9 +381,10 @@ __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
 
-// ABL (timing ablations only, results are garbage): 1 = no mainloop DMA (stage 0 reused),
+// ABL flags. Timing ablations (results are garbage): 1 = no mainloop DMA (stage 0 reused),
 // 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores.
-enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4 };
+// Option (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3.
+enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8 };
 
 template <class Cfg, int QT, int ABL = 0>
 __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __restrict__ A,
@@ -517,8 +518,88 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
   };
 
-  // ---- mainloop: stage s+1 in flight (LDS-DMA) while stage s is consumed ----
-  if (nst > 0) {
+  // ---- stagger (V2_STAGGER): SIMD partners are waves w and w+4 (a workgroup's waves go to the
+  // SIMDs cyclically). In lockstep both read LDS, then both issue MFMAs, then meet at the barrier.
+  // Waves 4-7 instead defer the second K half of every stage past the barrier, holding its
+  // fragments in registers: after each barrier they start on MFMAs while waves 0-3 start on LDS
+  // reads. Every accumulator still sees its K chunks in order -> bit-identical results.
+  if constexpr ((ABL & V2_STAGGER) != 0) {
+    typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
+    constexpr int SUBH = (QT == QT_I4) ? 2 : 1;  // MFMA K steps per 64-B half stage
+    struct Half {
+      word_t a[SUBH][FM];
+      word_t b[SUBH][FN];
+    };
+    auto hread = [&](Half& f, int buf, int h) {
+      const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
+      const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
+#pragma unroll
+      for (int t = 0; t < SUBH; ++t) {
+        const uint32_t off = QT == QT_I4
+                                 ? (uint32_t)(((2 * (2 * h + t) + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8)
+                                 : (uint32_t)(((h * 4 + g) ^ swz) << 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) f.a[t][i] = *reinterpret_cast<const word_t*>(As + i * 2048 + off);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) f.b[t][j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
+      }
+    };
+    auto hmma = [&](const Half& f) {
+#pragma unroll
+      for (int t = 0; t < SUBH; ++t) {
+        if constexpr (QT == QT_I4) {
+          v4i b[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) b[j] = widen_i4(f.b[t][j]);
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const v4i a = widen_i4(f.a[t][i]);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a, acc[i][j], 0, 0, 0);
+          }
+        } else if constexpr (QT == QT_I8) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.b[t][j], f.a[t][i], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, f.b[t][j]),
+                                                                 __builtin_bit_cast(v8h, f.a[t][i]), acc[i][j], 0, 0, 0);
+        }
+      }
+    };
+    if (nst > 0) {
+      Half fr;  // one fragment set (the late schedule carries it across the barrier)
+      issue(0, 0);
+      __syncthreads();
+      if (wave >= Cfg::WM * Cfg::WN / 2) {  // late: straight-line loop of its own
+        for (int s = 0; s < nst; ++s) {
+          if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
+          if (s > 0) hmma(fr);  // second half of stage s-1 (its buffer may be refilled now)
+          hread(fr, s & 1, 0);
+          hmma(fr);
+          hread(fr, s & 1, 1);  // landed before the barrier below (it waits lgkmcnt(0))
+          __syncthreads();
+        }
+        hmma(fr);
+      } else {
+        for (int s = 0; s < nst; ++s) {
+          if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
+          hread(fr, s & 1, 0);
+          hmma(fr);
+          hread(fr, s & 1, 1);
+          hmma(fr);
+          __syncthreads();
+        }
+      }
+    }
+  } else if (nst > 0) {
+    // ---- mainloop: stage s+1 in flight (LDS-DMA) while stage s is consumed ----
     issue(0, 0);
     __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
     for (int s = 0; s < nst; ++s) {
@@ -600,7 +681,7 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     if (tall) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  } else if constexpr (ABL != 0) {
+  } else if constexpr ((ABL & 7) != 0) {
     return;  // ablation builds time the int8 path only
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
     if (tall) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);

@@ -65,7 +65,7 @@ def test_struct_plan_info_layout():
 
 
 def test_auto_variant_follows_quant_mix():
-    """MXMOE_GG_VARIANT_AUTO: int4 present -> the 256x128 variant, else the default (256x256)."""
+    """MXMOE_GG_VARIANT_AUTO: only w4a4 -> the 256x128 variant, else the default (256x256)."""
     names = [ln.split()[1] for ln in nat.list_variants()]
     int4_v = names.index("v3_256x128_w4_dma_ring3_2wg")
 
@@ -73,13 +73,16 @@ def test_auto_variant_follows_quant_mix():
         arr = (nat.GGProblemC * len(ps))(*ps)
         return nat.workspace_size(arr, len(ps), v)
 
+    assert names[nat.default_variant()] == "v2s_256x256_w8_dma_stagger"
     big = dict(M=4096, N=4096, K=1024)
     w8 = [_prob(**big)]
+    w4 = [_prob(a_bits=4, w_bits=4, **big)] * 2
     mix = [_prob(**big), _prob(a_bits=4, w_bits=4, **big)]
     assert ws(w8, nat.VARIANT_AUTO) == ws(w8, nat.default_variant())
-    assert ws(mix, nat.VARIANT_AUTO) == ws(mix, int4_v) != ws(mix, nat.default_variant())
-    # an empty int4 problem does not count
-    assert ws(w8 + [_prob(a_bits=4, w_bits=4, M=0)], nat.VARIANT_AUTO) == ws(w8 + [_prob(M=0)], nat.default_variant())
+    assert ws(mix, nat.VARIANT_AUTO) == ws(mix, nat.default_variant())
+    assert ws(w4, nat.VARIANT_AUTO) == ws(w4, int4_v) != ws(w4, nat.default_variant())
+    # an empty problem of another type does not count
+    assert ws(w4 + [_prob(M=0)], nat.VARIANT_AUTO) == ws(w4 + [_prob(M=0)], int4_v)
 
 
 def _plan(problems, ws_bytes=1 << 20):
