@@ -150,6 +150,7 @@ Variant make_v2(const char* name) {
   return v;
 }
 
+
 typedef TileCfg<128, 128, 2, 2, 2> T128x128;
 typedef TileCfg<256, 128, 2, 2, 1> T256x128;
 typedef TileCfg<128, 256, 2, 2, 1> T128x256;

@@ -386,6 +386,61 @@ __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
 // Option (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3.
 enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8 };
 
+// One 64-B K half of a v2 stage (128-B rows, XOR-swizzled 16-B chunks) as raw fragment words:
+// read from LDS, then consumed by the MFMAs (int4 widened at use). Used by the staggered v2
+// mainloop (gg_tile_v2 with V2_STAGGER).
+template <class Cfg, int QT>
+struct V2Half {
+  typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
+  static constexpr int FM = Cfg::FM, FN = Cfg::FN;
+  static constexpr int SUBH = (QT == QT_I4) ? 2 : 1;  // MFMA K steps per 64-B half stage
+  word_t a[SUBH][FM];
+  word_t b[SUBH][FN];
+
+  __device__ __forceinline__ void read(const uint8_t* stage, uint32_t a_row, uint32_t b_row, int swz, int g, int h) {
+    const uint8_t* As = stage + a_row;
+    const uint8_t* Bs = stage + Cfg::A_BYTES + b_row;
+#pragma unroll
+    for (int t = 0; t < SUBH; ++t) {
+      const uint32_t off = QT == QT_I4 ? (uint32_t)(((2 * (2 * h + t) + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8)
+                                       : (uint32_t)(((h * 4 + g) ^ swz) << 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[t][i] = *reinterpret_cast<const word_t*>(As + i * 2048 + off);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[t][j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
+    }
+  }
+  __device__ __forceinline__ void mma(typename AccT<QT>::type (&acc)[FM][FN]) const {
+#pragma unroll
+    for (int t = 0; t < SUBH; ++t) {
+      if constexpr (QT == QT_I4) {
+        v4i bw[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bw[j] = widen_i4(b[t][j]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const v4i aw = widen_i4(a[t][i]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bw[j], aw, acc[i][j], 0, 0, 0);
+        }
+      } else if constexpr (QT == QT_I8) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[t][j], a[t][i], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, b[t][j]),
+                                                               __builtin_bit_cast(v8h, a[t][i]), acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+};
+
 template <class Cfg, int QT, int ABL = 0>
 __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
@@ -524,55 +579,9 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   // fragments in registers: after each barrier they start on MFMAs while waves 0-3 start on LDS
   // reads. Every accumulator still sees its K chunks in order -> bit-identical results.
   if constexpr ((ABL & V2_STAGGER) != 0) {
-    typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
-    constexpr int SUBH = (QT == QT_I4) ? 2 : 1;  // MFMA K steps per 64-B half stage
-    struct Half {
-      word_t a[SUBH][FM];
-      word_t b[SUBH][FN];
-    };
-    auto hread = [&](Half& f, int buf, int h) {
-      const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
-      const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
-#pragma unroll
-      for (int t = 0; t < SUBH; ++t) {
-        const uint32_t off = QT == QT_I4
-                                 ? (uint32_t)(((2 * (2 * h + t) + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8)
-                                 : (uint32_t)(((h * 4 + g) ^ swz) << 4);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) f.a[t][i] = *reinterpret_cast<const word_t*>(As + i * 2048 + off);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) f.b[t][j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
-      }
-    };
-    auto hmma = [&](const Half& f) {
-#pragma unroll
-      for (int t = 0; t < SUBH; ++t) {
-        if constexpr (QT == QT_I4) {
-          v4i b[FN];
-#pragma unroll
-          for (int j = 0; j < FN; ++j) b[j] = widen_i4(f.b[t][j]);
-#pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            const v4i a = widen_i4(f.a[t][i]);
-#pragma unroll
-            for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a, acc[i][j], 0, 0, 0);
-          }
-        } else if constexpr (QT == QT_I8) {
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.b[t][j], f.a[t][i], acc[i][j], 0, 0, 0);
-        } else {
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, f.b[t][j]),
-                                                                 __builtin_bit_cast(v8h, f.a[t][i]), acc[i][j], 0, 0, 0);
-        }
-      }
-    };
+    typedef V2Half<Cfg, QT> Half;
+    auto hread = [&](Half& f, int buf, int h) { f.read(lds + buf * Cfg::STAGE_BYTES, a_row, b_row, swz, g, h); };
+    auto hmma = [&](const Half& f) { f.mma(acc); };
     if (nst > 0) {
       Half fr;  // one fragment set (the late schedule carries it across the barrier)
       issue(0, 0);
