@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="fp16", choices=list(CONFIGS))
+    ap.add_argument("--no-scaling-sim", action="store_true",
+                    help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
     ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extras", default="w8a8,mixed", help="other configs measured as extra fields (N=1)")
@@ -212,6 +214,26 @@ def main():
                          "down_tflops": round(r["flops"]["down"] / (r["per"]["down"]["median_ms"] * 1e-3) / 1e12, 2),
                          "roofline_frac": round(ff / (tt * 1e-3) / 1e12 / pk, 4), "peak_tflops": pk,
                          "variant": r["variant"]}
+
+    if world == 1 and not args.no_scaling_sim:
+        from mxmoe_amd.harness import build_layer_inputs as _bli, strong_scaling_sim, time_reference_abi
+
+        sim, asref = {}, {}
+        for gg in ("gate_up", "down"):
+            li = _bli(main_res["shapes"][gg], device=dev, seed=42 + (gg == "down"))
+            sim[gg] = strong_scaling_sim(li)
+            asref[gg] = round(time_reference_abi(li), 4)
+            del li
+            torch.cuda.empty_cache()
+        extras["strong_scaling_sim"] = {
+            "what": "compute-only T1 / max-rank T_G of dist.nslice_plan work lists, each timed on this one GPU "
+                    "(ranks are independent GPUs); C all-gather not included (bytes per rank listed)",
+            **sim}
+        f = main_res["flops"]
+        extras["as_reference"] = {
+            "what": "groupgemm_mxmoe (reference FuncType): per-call host plan + table upload + launch, wall ms",
+            "gate_up_ms": asref["gate_up"], "down_ms": asref["down"],
+            "tflops": round((f["gate_up"] + f["down"]) / ((asref["gate_up"] + asref["down"]) * 1e-3) / 1e12, 2)}
 
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:

@@ -102,3 +102,65 @@ def write_csv(path: str, rows: list[dict]) -> None:
         w.writerow(["kernel_name", "avg_time", "TFLOPS", "speedup"])
         for r in rows:
             w.writerow([r["kernel_name"], f"{r['avg_time']:.6f}", f"{r['TFLOPS']:.3f}", f"{r['speedup']:.3f}"])
+
+
+def slice_problem(p: Problem, n0: int, n1: int) -> Problem:
+    """Columns [n0, n1) of a problem as a strided view: B rows / scale_b entries n0..n1 (contiguous),
+    C columns n0..n1 (row stride = the full problem's ldc). No copy."""
+    return dataclasses.replace(p, B=p.B[n0:n1], C=p.C[:, n0:n1], N=n1 - n0, ldc=p.ldc or p.N,
+                               scale_b=None if p.scale_b is None else p.scale_b[n0:n1])
+
+
+def strong_scaling_sim(inputs: LayerInputs, worlds: Sequence[int] = (2, 4, 8), warmup: int = 5,
+                       iters: int = 20) -> dict:
+    """Compute-only strong scaling of one GroupGEMM call, measured on ONE GPU:
+    each rank's work list of dist.nslice_plan runs as its own planned call; ranks are independent
+    GPUs, so T_G = max over ranks of that time and speedup = T_1 / T_G. The C all-gather that
+    follows on a real node is reported separately as bytes per rank (not timed here)."""
+    from .dist import nslice_plan, shard_bytes
+
+    t1 = time_launches(GroupGemm(inputs.problems).launch, warmup, iters)["median_ms"]
+    out = {"t1_ms": round(t1, 4)}
+    for G in worlds:
+        plan = nslice_plan(inputs.shapes, G)
+        per_rank = []
+        for work in plan:
+            probs = [slice_problem(inputs.problems[w.problem], w.n0, w.n1) for w in work]
+            per_rank.append(time_launches(GroupGemm(probs).launch, warmup, iters)["median_ms"] if probs else 0.0)
+        tg = max(per_rank)
+        out[str(G)] = {"t_ms_max_rank": round(tg, 4), "speedup": round(t1 / tg, 3),
+                       "rank_ms": [round(x, 4) for x in per_rank],
+                       "allgather_MB_per_rank": round(2 * max(shard_bytes(inputs.shapes, w) for w in plan) / 1e6, 1)}
+    return out
+
+
+def time_reference_abi(inputs: LayerInputs, iters: int = 20) -> float:
+    """Wall ms per call of the reference-compatible entry (groupgemm_mxmoe: device pointer arrays,
+    per-call host planning + upload + launch, legacy stream) — the 'as-reference' number, comparable
+    with the reference host API that rebuilds its prefix array every call (kernel_sketch.py:87-143)."""
+    import time
+
+    from .groupgemm import groupgemm_reference_abi
+
+    dev = inputs.problems[0].C.device
+
+    def ptrs(get):
+        return torch.tensor([0 if get(p) is None else get(p).data_ptr() for p in inputs.problems],
+                            dtype=torch.int64, device=dev)
+
+    arrs = [ptrs(lambda p: p.A), ptrs(lambda p: p.B), ptrs(lambda p: p.scale_a), ptrs(lambda p: p.scale_b),
+            ptrs(lambda p: p.C)]
+    sizes = [(p.M, p.N, p.K) for p in inputs.problems]
+    qs = [p.q for p in inputs.problems]
+
+    def call():
+        groupgemm_reference_abi(*arrs, sizes, qs)
+
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        call()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / iters

@@ -11,5 +11,5 @@ timeout -k 10 400 python bench.py "$@" > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG
 cat $OUT/bench_$TAG.json
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-  python3 bench.py --no-cpu-baseline --extras "" "$@" > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err || exit $?
+  python3 bench.py --no-cpu-baseline --no-scaling-sim --extras "" "$@" > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err || exit $?
 find $OUT/prof_$TAG -name "*kernel_stats.csv" | head -1 | xargs cat

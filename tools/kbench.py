@@ -1,6 +1,7 @@
 """Launch one GroupGEMM call repeatedly (for rocprofv3 counter runs / A-B of variants).
 
 python tools/kbench.py --cfg w8a8 --gg gate_up --variants 0,3 --iters 20 [--only shared|routed|all]
+(--variants auto = the library's AUTO choice)
 """
 from __future__ import annotations
 
@@ -35,10 +36,10 @@ def main():
     elif args.only == "routed":
         shapes = shapes[:-1]
     inp = build_layer_inputs(shapes)
-    for v in [int(x) for x in args.variants.split(",")]:
-        gg = GroupGemm(inp.problems, variant=v)
+    for v in [None if x == "auto" else int(x) for x in args.variants.split(",")]:
+        gg = GroupGemm(inp.problems, variant=v)  # None: MXMOE_GG_VARIANT_AUTO
         t = time_launches(gg.launch, warmup=3, iters=args.iters)
-        print(json.dumps({"variant": v, "cfg": args.cfg, "gg": args.gg, "only": args.only,
+        print(json.dumps({"variant": gg.variant, "cfg": args.cfg, "gg": args.gg, "only": args.only,
                           "median_ms": round(t["median_ms"], 4), "tiles": gg.total_tiles, "grid": gg.info.grid,
                           "tflops": round(inp.flops / (t["median_ms"] * 1e-3) / 1e12, 1)}), flush=True)
 

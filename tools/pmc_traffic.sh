@@ -1,0 +1,41 @@
+#!/bin/bash
+# HBM traffic per bench step (gate_up + down launches of the AUTO variant) from rocprofv3 PMC,
+# collected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE and WRITE_SIZE in separate passes
+# (kernel-trace only, no other tracing), FETCH_SIZE doubled on gfx950, both reported in KB.
+# usage: bash tools/pmc_traffic.sh <cfg...>     -> gpurun_out/pmc_traffic/pmc_traffic.json
+set -o pipefail
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/pmc_traffic
+mkdir -p $OUT
+cd $REPO
+export TMPDIR=/tmp
+for cfg in "$@"; do
+  for gg in gate_up down; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 240 rocprofv3 --pmc $ctr --output-format csv -d $OUT/${cfg}_${gg}_${ctr} -o run -- \
+        python3 tools/kbench.py --cfg $cfg --gg $gg --variants auto --iters 10 > $OUT/${cfg}_${gg}_${ctr}.log 2>&1 || exit $?
+    done
+  done
+done
+python3 - "$OUT" "$@" <<'PY'
+import csv, glob, json, sys
+out, cfgs = sys.argv[1], sys.argv[2:]
+res = {}
+for cfg in cfgs:
+    d = {}
+    for gg in ("gate_up", "down"):
+        v = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            vals = [float(r["Counter_Value"]) for f in glob.glob(f"{out}/{cfg}_{gg}_{ctr}/**/*counter_collection.csv", recursive=True)
+                    for r in csv.DictReader(open(f)) if "gg_" in r.get("Kernel_Name", "") and r["Counter_Name"] == ctr]
+            v[ctr] = sum(vals) / len(vals)
+        kb = 2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]
+        d[gg] = {"fetch_bytes_x2": 2 * v["FETCH_SIZE"] * 1024, "write_bytes": v["WRITE_SIZE"] * 1024,
+                 "hbm_bytes": kb * 1024}
+    d["hbm_bytes_per_step"] = d["gate_up"]["hbm_bytes"] + d["down"]["hbm_bytes"]
+    res[cfg] = d
+res["_method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes over tools/kbench.py (AUTO variant), "
+                  "mean per dispatch, KB -> bytes, FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md §HBM)")
+json.dump(res, open(f"{out}/pmc_traffic.json", "w"), indent=1)
+print(json.dumps(res, indent=1))
+PY
