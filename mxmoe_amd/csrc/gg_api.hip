@@ -167,6 +167,10 @@ const std::vector<Variant>& variants() {
       make_v2<ABL_NO_EPI>("abl_v2_noepi"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
+      // timing ablations of the staggered v2 (WRONG RESULTS by design; int8 tiles only)
+      make_v2<V2_STAGGER | ABL_NO_DMA>("abl_v2s_nodma"),
+      make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
+      make_v2<V2_STAGGER | ABL_NO_DMA | ABL_NO_EPI>("abl_v2s_nodma_noepi"),
   };
   return v;
 }

@@ -381,6 +381,20 @@ __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS barrier that lets LDS-DMA stay in flight: drain this wave's LDS reads, barrier, and keep the
+// compiler from moving LDS accesses across it (the "memory" clobbers) — unlike __syncthreads(),
+// no vmcnt(0).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ABL flags. Timing ablations (results are garbage): 1 = no mainloop DMA (stage 0 reused),
 // 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores.
 // Option (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3.
@@ -582,10 +596,11 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     typedef V2Half<Cfg, QT> Half;
     auto hread = [&](Half& f, int buf, int h) { f.read(lds + buf * Cfg::STAGE_BYTES, a_row, b_row, swz, g, h); };
     auto hmma = [&](const Half& f) { f.mma(acc); };
+    auto stage_sync = [&](int) { __syncthreads(); };  // stage s+1 landed, buffer s&1 released
     if (nst > 0) {
       Half fr;  // one fragment set (the late schedule carries it across the barrier)
       issue(0, 0);
-      __syncthreads();
+      stage_sync(-1);
       if (wave >= Cfg::WM * Cfg::WN / 2) {  // late: straight-line loop of its own
         for (int s = 0; s < nst; ++s) {
           if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
@@ -593,7 +608,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           hread(fr, s & 1, 0);
           hmma(fr);
           hread(fr, s & 1, 1);  // landed before the barrier below (it waits lgkmcnt(0))
-          __syncthreads();
+          stage_sync(s);
         }
         hmma(fr);
       } else {
@@ -603,7 +618,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           hmma(fr);
           hread(fr, s & 1, 1);
           hmma(fr);
-          __syncthreads();
+          stage_sync(s);
         }
       }
     }
@@ -733,19 +748,6 @@ struct V3Cfg {
 
 __device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }  // T = {0,2,3,1}
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// LDS barrier that lets LDS-DMA stay in flight: drain this wave's LDS reads, barrier, and keep the
-// compiler from moving LDS accesses across it (the "memory" clobbers) — unlike __syncthreads(),
-// no vmcnt(0).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // Epilogue shared by v3 / v4: dequant (int paths) + fp16 rounding, per-wave LDS staging of the
 // WTM x WTN fp16 sub-tile in XOR-swizzled 16-B chunks, then 16-B row stores (coalesced along N).

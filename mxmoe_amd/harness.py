@@ -112,21 +112,22 @@ def slice_problem(p: Problem, n0: int, n1: int) -> Problem:
 
 
 def strong_scaling_sim(inputs: LayerInputs, worlds: Sequence[int] = (2, 4, 8), warmup: int = 5,
-                       iters: int = 20) -> dict:
+                       iters: int = 20, variant: Optional[int] = None) -> dict:
     """Compute-only strong scaling of one GroupGEMM call, measured on ONE GPU:
     each rank's work list of dist.nslice_plan runs as its own planned call; ranks are independent
     GPUs, so T_G = max over ranks of that time and speedup = T_1 / T_G. The C all-gather that
     follows on a real node is reported separately as bytes per rank (not timed here)."""
     from .dist import nslice_plan, shard_bytes
 
-    t1 = time_launches(GroupGemm(inputs.problems).launch, warmup, iters)["median_ms"]
+    t1 = time_launches(GroupGemm(inputs.problems, variant=variant).launch, warmup, iters)["median_ms"]
     out = {"t1_ms": round(t1, 4)}
     for G in worlds:
         plan = nslice_plan(inputs.shapes, G)
         per_rank = []
         for work in plan:
             probs = [slice_problem(inputs.problems[w.problem], w.n0, w.n1) for w in work]
-            per_rank.append(time_launches(GroupGemm(probs).launch, warmup, iters)["median_ms"] if probs else 0.0)
+            per_rank.append(time_launches(GroupGemm(probs, variant=variant).launch, warmup, iters)["median_ms"]
+                            if probs else 0.0)
         tg = max(per_rank)
         out[str(G)] = {"t_ms_max_rank": round(tg, 4), "speedup": round(t1 / tg, 3),
                        "rank_ms": [round(x, 4) for x in per_rank],

@@ -8,7 +8,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -27,6 +29,8 @@ def main():
     ap.add_argument("--variants", default="0,3")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="all", choices=["all", "shared", "routed"])
+    ap.add_argument("--rounds", type=int, default=5, help="round-robin rounds over the variants")
+    ap.add_argument("--settle-s", type=float, default=1.0, help="seconds of load before timing")
     args = ap.parse_args()
     kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
           "mixed": dict(qconfig=mixed_qconfig_lp1())}[args.cfg]
@@ -36,12 +40,27 @@ def main():
     elif args.only == "routed":
         shapes = shapes[:-1]
     inp = build_layer_inputs(shapes)
-    for v in [None if x == "auto" else int(x) for x in args.variants.split(",")]:
-        gg = GroupGemm(inp.problems, variant=v)  # None: MXMOE_GG_VARIANT_AUTO
-        t = time_launches(gg.launch, warmup=3, iters=args.iters)
+    ggs = [GroupGemm(inp.problems, variant=None if x == "auto" else int(x))  # None: MXMOE_GG_VARIANT_AUTO
+           for x in args.variants.split(",")]
+    # A/B without order bias: ~1 s of sustained load first (clocks settle), then round-robin rounds
+    # over the variants; per-variant median over every round's samples
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.settle_s:
+        for gg in ggs:
+            gg.launch()
+        torch.cuda.synchronize()
+    samples = [[] for _ in ggs]
+    per_round = max(1, args.iters // args.rounds)
+    for _ in range(args.rounds):
+        for k, gg in enumerate(ggs):
+            t = time_launches(gg.launch, warmup=1, iters=per_round)
+            samples[k].append(t["median_ms"])
+    for gg, ts in zip(ggs, samples):
+        med = statistics.median(ts)
         print(json.dumps({"variant": gg.variant, "cfg": args.cfg, "gg": args.gg, "only": args.only,
-                          "median_ms": round(t["median_ms"], 4), "tiles": gg.total_tiles, "grid": gg.info.grid,
-                          "tflops": round(inp.flops / (t["median_ms"] * 1e-3) / 1e12, 1)}), flush=True)
+                          "median_ms": round(med, 4), "spread_ms": round(max(ts) - min(ts), 4),
+                          "tiles": gg.total_tiles, "grid": gg.info.grid,
+                          "tflops": round(inp.flops / (med * 1e-3) / 1e12, 1)}), flush=True)
 
 
 if __name__ == "__main__":
