@@ -38,6 +38,8 @@ CONFIGS = {
                  name="qwen2_moe layer-11 w4a4_g-1_sym GroupGEMM bs=8192 (int8 MFMA)"),
     "mixed": dict(kw="mixed", peak="int8", dtype="int4+int8",
                   name="qwen2_moe layer-11 mixed w4a4+w8a8 (wbits=5.0, LP-1 qconfig) bs=8192"),
+    "ds2_mixed": dict(kw="ds2_mixed", peak="int8", dtype="int4+int8",
+                      name="DeepSeek-V2-Lite MoE layer mixed w4a4+w8a8 (25 % w8a8 units) bs=8192, 64 experts"),
 }
 
 
@@ -48,13 +50,91 @@ def log(*a):
 def layer_shapes(cfg: str, world: int, rank: int, bs: int = 8192):
     """Per-rank problem lists {gate_up, down} (expert-parallel weak scaling, mxmoe_amd/dist.py)."""
     from mxmoe_amd.dist import ep_shard
-    from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+
+    return ep_shard(full_layer(cfg, bs), world, rank)
+
+
+def full_layer(cfg: str, bs: int = 8192):
+    """The config's whole layer {gate_up, down} (one GPU's worth at N = 1)."""
+    from mxmoe_amd.workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1,
+                                    qwen2_layer11_workload)
 
     kw = CONFIGS[cfg]["kw"]
+    if kw == "ds2_mixed":
+        return load_workload(ds2_workload(bs, qconfig=ds2_mixed_qconfig()))["layer-1"]
     if kw == "mixed":
         kw = dict(qconfig=mixed_qconfig_lp1())
-    wl = load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
-    return ep_shard(wl, world, rank)
+    return load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
+
+
+def strong_scaling_rccl(cfg: str, dev, world: int, rank: int, steps: int = 10, warmup: int = 3, coll_dev=None) -> dict:
+    """Strong scaling of one layer's calls over the node, measured for real at N > 1:
+    every rank holds the full inputs (activations and weights replicated, same seeds), runs its
+    dist.nslice_plan work list with each C slice written straight into a packed local shard, then
+    one all_gather_into_tensor over RCCL / xGMI. Reports T1 (the full call on each GPU, max over
+    ranks), compute-only time (max over ranks) and compute + all-gather."""
+    import dataclasses
+    import time
+
+    import torch.distributed as dist
+
+    from mxmoe_amd.dist import nslice_plan, shard_bytes
+    from mxmoe_amd.groupgemm import GroupGemm
+    from mxmoe_amd.harness import build_layer_inputs
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        t = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], dtype=torch.float64, device=coll_dev or dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    out = {}
+    layer = full_layer(cfg)
+    for gg in ("gate_up", "down"):
+        inp = build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down"))
+        full = GroupGemm(inp.problems, device=dev)
+        t1 = timed(full.launch)
+        plan = nslice_plan(inp.shapes, world)
+        pad = max(shard_bytes(inp.shapes, w) for w in plan)
+        local = torch.empty(pad, dtype=torch.float16, device=dev)
+        gathered = torch.empty(world * pad, dtype=torch.float16, device=dev)
+        mine, off = [], 0
+        for w in plan[rank]:
+            p = inp.problems[w.problem]
+            n = p.M * w.width
+            mine.append(dataclasses.replace(p, B=p.B[w.n0:w.n1], N=w.width, ldc=0,
+                                            C=local[off:off + n].view(max(p.M, 1), w.width),
+                                            scale_b=None if p.scale_b is None else p.scale_b[w.n0:w.n1]))
+            off += n
+        part = GroupGemm(mine, device=dev) if mine else None
+
+        def compute():
+            if part is not None:
+                part.launch()
+
+        def e2e():
+            compute()
+            if (coll_dev or dev).type == "cuda":
+                dist.all_gather_into_tensor(gathered, local)
+            else:  # gloo rehearsal: stage through host memory
+                g = torch.empty(gathered.numel(), dtype=gathered.dtype)
+                dist.all_gather_into_tensor(g, local.cpu())
+                gathered.copy_(g)
+
+        tc, te = timed(compute), timed(e2e)
+        out[gg] = {"t1_ms": round(t1, 4), "compute_ms": round(tc, 4), "compute_allgather_ms": round(te, 4),
+                   "speedup_compute": round(t1 / tc, 3), "speedup_with_allgather": round(t1 / te, 3),
+                   "allgather_MB_per_rank": round(2 * pad / 1e6, 1)}
+        del inp, full, part, local, gathered
+        torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(cfg: str, shapes, budget_s: float = 15.0) -> dict:
@@ -116,20 +196,29 @@ def main():
                     help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
     ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extras", default="w8a8,mixed", help="other configs measured as extra fields (N=1)")
+    ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 strong-scaling + all-gather extra")
+    ap.add_argument("--extras", default="w8a8,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MXMOE_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU (collectives
+    # staged through host memory); the node runs use RCCL ("nccl")
+    backend = os.environ.get("MXMOE_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
 
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")  # where small collective tensors live
 
     from mxmoe_amd import _native as nat
     from mxmoe_amd.groupgemm import GroupGemm
@@ -164,10 +253,10 @@ def main():
             dt = time.perf_counter() - t0
             if world > 1:
                 torch.distributed.barrier()
-                t = torch.tensor([dt], device=dev, dtype=torch.float64)
+                t = torch.tensor([dt], device=coll_dev, dtype=torch.float64)
                 torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
                 dt = float(t.item())
-                f = torch.tensor([float(flops["gate_up"] + flops["down"])], device=dev, dtype=torch.float64)
+                f = torch.tensor([float(flops["gate_up"] + flops["down"])], device=coll_dev, dtype=torch.float64)
                 torch.distributed.all_reduce(f)
                 total_flops = float(f.item())
             else:
@@ -191,7 +280,7 @@ def main():
     t_gu, t_dn = per["gate_up"]["mean_ms"], per["down"]["mean_ms"]
     achieved = (f_gu + f_dn) / ((t_gu + t_dn) * 1e-3) / 1e12
     value = main_res["total_flops"] * args.steps / main_res["dt"] / 1e12
-    pmc = load_pmc_traffic(cfg)
+    pmc = load_pmc_traffic(cfg) if world == 1 else None  # the committed PMC passes are single-GPU runs
 
     extras = {}
     if rank == 0:
@@ -235,6 +324,16 @@ def main():
             "gate_up_ms": asref["gate_up"], "down_ms": asref["down"],
             "tflops": round((f["gate_up"] + f["down"]) / ((asref["gate_up"] + asref["down"]) * 1e-3) / 1e12, 2)}
 
+    if world > 1 and not args.no_strong_scaling:
+        try:
+            extras["strong_scaling_rccl"] = {
+                "what": "one layer's calls split by dist.nslice_plan over the node: T1 = full call per GPU, "
+                        "compute = max-rank time of the local work list, + RCCL all_gather_into_tensor of "
+                        "the packed C shards (wall ms, max over ranks)",
+                **strong_scaling_rccl(cfg, dev, world, rank, coll_dev=coll_dev)}
+        except Exception as e:  # a failure here must not lose the weak-scaling line
+            extras["strong_scaling_rccl"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, main_res["shapes"])
@@ -253,9 +352,12 @@ def main():
             "vs_baseline": None,
             "dtype": CONFIGS[cfg]["dtype"],
             "data": "synthetic: uniform(-1,1) fp16 inputs (seeded) -> RTN per-row quantised + pack_wxax for "
-                    "quantised problems; routed M_e = reference's committed bs=8192 histogram",
+                    "quantised problems; routed M_e = " + ("reference's committed bs=8192 histogram"
+                                                         if not cfg.startswith("ds2") else
+                                                         "seeded multinomial (SURVEY.md 8d)"),
             "config": {"workload": CONFIGS[cfg]["name"] + (f", expert-parallel over {world} GPUs" if world > 1 else ""),
-                       "model": "qwen2_moe (Qwen1.5-MoE-A2.7B) MoE GroupGEMMs", "global_batch": 8192 * world,
+                       "model": ("DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")
+                       + " MoE GroupGEMMs", "global_batch": 8192 * world,
                        "seq_len": None, "parallelism": f"ep{world}" if world > 1 else "single",
                        "problems_per_call": len(main_res["shapes"]["gate_up"]), "variant": main_res["variant"],
                        "variant_name": nat.list_variants()[main_res["variant"]].split()[1]},

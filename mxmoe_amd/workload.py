@@ -205,6 +205,37 @@ def ds2_workload(bs: int = 8192, qconfig: Optional[dict] = None, qstr: Optional[
     return generate_workload_from_trace(ds2_trace(bs, seed), bs, 1, qconfig=qconfig, qstr=qstr)
 
 
+def ds2_mixed_qconfig(seed: int = 0, frac: float = 0.25, layer: int = 1) -> dict:
+    """DeepSeek-V2-Lite mixed w4a4 + w8a8 allocation (the reference ships no qconfig
+    for this model): a seeded (PCG64) random order of (expert, gate_up | down) blocks is scanned
+    greedily, each block turned w8a8 while the w8a8 weight units stay <= frac of all units; units per
+    linear are 1 (routed) or 2 (shared expert, index E), gate and up tied. Export format of
+    bits_solver.py:25-71. Pinned by tests/golden/ds2_mixed_alloc.json."""
+    E = MODEL_SHAPES["ds2"]["E"]
+    blocks = [(e, lin) for e in range(E + 1) for lin in ("gate_up", "down")]
+
+    def units(e: int, lin: str) -> int:
+        return (2 if e == E else 1) * (2 if lin == "gate_up" else 1)
+
+    budget = frac * sum(units(*b) for b in blocks)
+    w8, used = set(), 0
+    for i in np.random.default_rng(seed).permutation(len(blocks)):
+        b = blocks[int(i)]
+        if used + units(*b) <= budget:
+            w8.add(b)
+            used += units(*b)
+
+    def cfg(bits: int) -> dict:
+        return {"w_bits": bits, "w_gsize": -1, "w_sym": True, "w_clip": [1.0, 1.0],
+                "a_bits": bits, "a_gsize": -1, "a_sym": True, "a_clip": [1.0, 1.0]}
+
+    experts = {}
+    for e in range(E + 1):
+        gu, dn = (8 if (e, "gate_up") in w8 else 4), (8 if (e, "down") in w8 else 4)
+        experts[str(e)] = {"gate": cfg(gu), "up": cfg(gu), "down": cfg(dn)}
+    return {str(layer): {"experts": experts}}
+
+
 def mixed_qconfig_lp1() -> dict:
     """The committed mixed w4a4+w8a8 (wbits 5.0) qconfig solved from the reference's bits_model-1.lp."""
     return load_qconfig(WORKLOAD_DIR / "qconfig_qwen2_moe_w4a4+w8a8_wbits5.0_lp1.json")

@@ -121,3 +121,18 @@ def test_cli_workload_step(tmp_path, monkeypatch):
     assert cli.workload_suffix(A)[0] == "-fp16.json"
     t = cli.find_trace("qwen2_moe", "wiki2", 11, None)
     assert t["topk"] == 4 and len(t["layer-11"]["access_freq"]) == 60 and len([k for k in t if k.startswith("layer-")]) == 24
+
+
+def test_ds2_mixed_allocation_pinned():
+    """DeepSeek-V2-Lite mixed config: seeded greedy w8a8 pick up to 25 % of units."""
+    g = json.loads((GOLD / "ds2_mixed_alloc.json").read_text())
+    ex = wl.ds2_mixed_qconfig()["1"]["experts"]
+    assert len(ex) == 65 and all(c["gate"] == c["up"] for c in ex.values())
+    assert sorted(int(e) for e, c in ex.items() if c["gate"]["w_bits"] == 8) == g["w8a8_gate_up"]
+    assert sorted(int(e) for e, c in ex.items() if c["down"]["w_bits"] == 8) == g["w8a8_down"]
+    units = sum((2 if e == "64" else 1) * (2 if lin == "gate" else 1)
+                for e, c in ex.items() for lin in ("gate", "down") if c[lin]["w_bits"] == 8)
+    assert units == g["units_w8a8"] <= 0.25 * (64 * 3 + 2 * 3)
+    layer = wl.load_workload(wl.ds2_workload(8192, qconfig=wl.ds2_mixed_qconfig()))["layer-1"]
+    assert sum(p.M for p in layer["gate_up"][:-1]) == 8192 * 6 and layer["gate_up"][-1].shape == [8192, 5632, 2048]
+    assert layer["down"][-1].shape == [8192, 2048, 2816]
