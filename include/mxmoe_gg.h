@@ -143,6 +143,16 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
                     mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
                     mxmoe_qparams* h_qbits_list, int problem_count);
 
+/* Weight-only (WxA16) B, host-side and once per weight: converts the reference's packed words
+ * (pack_weightonly after permute_weight(Row), quantize.cuh:318-421: uint16 [N / (16/w_bits)][K],
+ * sym codes stored with the +2^(w_bits-1)-1 offset) into the layout the kernels read:
+ * uint8 [N][K * w_bits / 8], per 64-K segment of a row the K values {kc*32 + g*8 + e} at element
+ * position g*16 + kc*8 + e (kc < 2, g < 4, e < 8), 4-bit codes low nibble first. Code values are
+ * unchanged. Needs N % (8 * 16 / w_bits) == 0 and K % 64 == 0; w_bits 4 or 8. The scale / zero
+ * buffer is used as the reference lays it out (permute_scale: [K/gsize][N] sym, [K/gsize][N][2]
+ * scale/zp pairs asym). */
+int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bits, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,7 +74,7 @@ EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
     "mxmoe_gg_variant_tile", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
-    "groupgemm_mxmoe",
+    "groupgemm_mxmoe", "mxmoe_gg_repack_weightonly",
 )
 
 _lib = None
@@ -106,6 +106,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.groupgemm_mxmoe.restype = c.c_int
     lib.groupgemm_mxmoe.argtypes = [c.c_void_p] * 10 + [c.c_void_p, c.POINTER(MxmoeDim3), c.c_void_p,
                                                          c.POINTER(MxmoeQParams), c.c_int]
+    lib.mxmoe_gg_repack_weightonly.restype = c.c_int
+    lib.mxmoe_gg_repack_weightonly.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
 
 
 def lib() -> ctypes.CDLL:
@@ -156,6 +158,17 @@ def variant_tile(variant: int, a_bits: int, w_bits: int) -> dict:
     v = [ctypes.c_int32() for _ in range(4)]
     check(lib().mxmoe_gg_variant_tile(variant, a_bits, w_bits, *[ctypes.byref(x) for x in v]))
     return {"BM": v[0].value, "BN": v[1].value, "BK_bytes": v[2].value, "threads": v[3].value}
+
+
+def repack_weightonly(ref_words, N: int, K: int, w_bits: int):
+    """Reference weight-only packed words (numpy uint16 [N*w_bits/16, K], host) -> the kernel's
+    uint8 [N, K*w_bits/8] layout (mxmoe_gg_repack_weightonly)."""
+    import numpy as np
+
+    src = np.ascontiguousarray(ref_words, dtype=np.uint16)
+    out = np.empty((N, K * w_bits // 8), dtype=np.uint8)
+    check(lib().mxmoe_gg_repack_weightonly(src.ctypes.data, N, K, w_bits, out.ctypes.data))
+    return out
 
 
 def workspace_size(problems, problem_count: int, variant: int) -> int:

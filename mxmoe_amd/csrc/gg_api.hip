@@ -76,12 +76,15 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   if constexpr ((ABL & 7) != 0) {
     launch_v2_q<ABL, 7>(a, grid, s);
   } else {
-    switch (qmask & 7) {
+    switch (qmask & 31) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
       case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
       case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
       case 6: launch_v2_q<ABL, 6>(a, grid, s); break;
-      default: launch_v2_q<ABL, 7>(a, grid, s); break;
+      case 7: launch_v2_q<ABL, 7>(a, grid, s); break;
+      case 8: launch_v2_q<ABL, 8>(a, grid, s); break;    // w4a16 only
+      case 16: launch_v2_q<ABL, 16>(a, grid, s); break;  // w8a16 only
+      default: launch_v2_q<ABL, 31>(a, grid, s); break;
     }
   }
 }
@@ -110,6 +113,7 @@ Variant make_v0(const char* name) {
   v.geom[QT_F16] = {C16::BM, C16::BN, C16::BKB, C16::kThreads};
   v.geom[QT_I8] = {C8::BM, C8::BN, C8::BKB, C8::kThreads};
   v.geom[QT_I4] = {C4::BM, C4::BN, C4::BKB, C4::kThreads};
+  v.geom[QT_W4A16] = v.geom[QT_W8A16] = {0, 0, 0, 0};  // weight-only: v2 kernels only
   v.threads = C16::kThreads;
   v.lds_bytes = FusedCfg<C16, C8, C4>::LDS_BYTES;
   v.chunk = FusedCfg<C16, C8, C4>::LDS_BYTES <= 80 * 1024 ? 64 : 32;  // workgroups per XCD at once
@@ -126,6 +130,7 @@ Variant make_v3(const char* name) {
   v.name = name;
   v.kind = Kind::V3;
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};
+  v.geom[QT_W4A16] = v.geom[QT_W8A16] = {0, 0, 0, 0};  // weight-only: v2 kernels only
   v.threads = CT::NT;
   v.lds_bytes = CT::LDS_BYTES;
   v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
@@ -141,6 +146,8 @@ Variant make_v2(const char* name) {
   v.name = name;
   v.kind = Kind::V2;
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 128, 512};
+  v.geom[QT_W4A16] = {256, 256, 32, 512};  // 64-K stages: 32 B of 4-bit codes per row
+  v.geom[QT_W8A16] = {256, 256, 64, 512};
   v.threads = 512;
   v.lds_bytes = V2Cfg<256>::LDS_BYTES;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
@@ -199,6 +206,10 @@ int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
     *qt = QT_I4;
     return MXMOE_GG_OK;
   }
+  if (a_bits == 16 && (w_bits == 4 || w_bits == 8)) {  // weight-only; group size checked per problem
+    *qt = w_bits == 4 ? QT_W4A16 : QT_W8A16;
+    return MXMOE_GG_OK;
+  }
   return fail(MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported: w%da%d_g%d_%s", w_bits, a_bits, gsize,
               sym ? "sym" : "asym");
 }
@@ -226,11 +237,53 @@ WsLayout ws_layout(int P, int grid) {
 }
 
 // Validate one problem and fill its table row.
+// Weight-only WxA16: A fp16 [M][K], B codes [N][K * w_bits / 8] (mxmoe_gg_repack_weightonly
+// layout), scale_b = scale / zp in the reference permute_scale layout; K in 64-element stages.
+int build_meta_weightonly(const HostProblem& p, int idx, int qt, const Variant& v, bool check_ptrs, GGMeta* m) {
+  if (p.K % 64) return fail(MXMOE_GG_ERR_INVALID, "problem %d: weight-only needs K %% 64 == 0 (K=%d)", idx, p.K);
+  if (p.gsize != -1 && (p.gsize <= 0 || p.gsize % 64 || p.K % p.gsize))
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: weight-only group size %d must be -1 or a multiple of 64 dividing K=%d",
+                idx, p.gsize, p.K);
+  if (p.N % 8 != 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: N=%d must be a multiple of 8", idx, p.N);
+  const int64_t arow = (int64_t)p.K * 2, brow = (int64_t)p.K * p.w_bits / 8;
+  const int64_t lda_b = p.lda ? p.lda * 2 : arow;
+  const int64_t ldb_b = p.ldb ? p.ldb * 2 : brow;
+  const int64_t ldc = p.ldc ? p.ldc : p.N;
+  if (lda_b < arow || ldb_b < brow || (lda_b % 16) || (ldb_b % 16))
+    return fail(MXMOE_GG_ERR_INVALID, "problem %d: lda/ldb must be >= K row and a multiple of 8 words", idx);
+  if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
+  if (check_ptrs && p.M > 0 && p.N > 0) {
+    if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
+    if (!p.SB) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer (weight-only scale_b)", idx);
+    if (((uintptr_t)p.A | (uintptr_t)p.B | (uintptr_t)p.C) & 15)
+      return fail(MXMOE_GG_ERR_INVALID, "problem %d: A/B/C must be 16-byte aligned", idx);
+    if (((uintptr_t)p.SB) & (p.sym ? 1 : 3))
+      return fail(MXMOE_GG_ERR_INVALID, "problem %d: scales must be %d-byte aligned", idx, p.sym ? 2 : 4);
+  }
+  memset(m, 0, sizeof(*m));
+  m->M = p.M;
+  m->N = p.N;
+  m->K = p.K;
+  m->qtype = qt;
+  m->tiles_n = (p.N + v.geom[qt].bn - 1) / v.geom[qt].bn;
+  m->kbytes = (int32_t)arow;
+  m->reserved = p.gsize == -1 ? std::max(1, p.K / 64) : p.gsize / 64;  // 64-K stages per scale group
+  m->reserved2 = p.sym ? 1 : 0;
+  m->lda_b = lda_b;
+  m->ldb_b = ldb_b;
+  m->ldc = ldc;
+  return MXMOE_GG_OK;
+}
+
 int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs, GGMeta* m) {
   if (p.M < 0 || p.N < 0 || p.K < 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: negative shape", idx);
   int qt = 0;
   int st = qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt);
   if (st) return fail(st, "problem %d: %s", idx, g_last_error.c_str());
+  if (v.geom[qt].bn == 0)
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s does not implement w%da%d (quant type not supported)",
+                idx, v.name, p.w_bits, p.a_bits);
+  if (qt == QT_W4A16 || qt == QT_W8A16) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
   const int abits = qt == QT_F16 ? 16 : p.a_bits;
   const int64_t kbits = (int64_t)p.K * abits;
   if (kbits % 128 != 0)
@@ -417,7 +470,9 @@ int mxmoe_gg_variant_count(void) { return (int)variants().size(); }
 int mxmoe_gg_default_variant(void) { return variant_index(kDefaultVariantName); }
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
-  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym"};
+  // weight-only kernels cover every group size / sym of a bit width: listed under the base name
+  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16", "w8a16"};
+  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8};
   std::string out;
   const auto& vs = variants();
   for (size_t i = 0; i < vs.size(); ++i) {
@@ -425,7 +480,8 @@ int mxmoe_gg_list_variants(char* buf, size_t n) {
     int off = snprintf(line, sizeof(line), "%zu %s", i, vs[i].name);
     for (int q = 0; q < QT_COUNT; ++q) {
       const TileGeom& g = vs[i].geom[q];
-      const int bits = q == QT_F16 ? 16 : (q == QT_I8 ? 8 : 4);
+      if (g.bn == 0) continue;  // quant type not implemented by this variant
+      const int bits = wbits[q];
       const int waves = g.threads / 64;
       const int wm = 2, wn = waves / wm;
       off += snprintf(line + off, sizeof(line) - off,
@@ -583,6 +639,70 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
   mxmoe_gg_plan_info info;
   fill_info(plan, variant, l, ws, &info);
   return mxmoe_gg_launch(&info, nullptr);
+}
+
+
+// Inverse of the reference's permute_weight(Row) + pack_weightonly (quantize.cuh:318-421), then
+// the kernel layout (include/mxmoe_gg.h). Host code, run once per weight at load time.
+int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bits, uint8_t* out) {
+  if (!ref_words || !out || N <= 0 || K <= 0)
+    return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_repack_weightonly");
+  if (w_bits != 4 && w_bits != 8)
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "weight-only repack: w_bits must be 4 or 8 (got %d)", w_bits);
+  const int pack = 16 / w_bits, mask = (1 << w_bits) - 1;
+  if (N % (pack * 8) || K % 64)
+    return fail(MXMOE_GG_ERR_INVALID, "weight-only repack: need N %% %d == 0 and K %% 64 == 0 (N=%d, K=%d)",
+                pack * 8, N, K);
+  // 1. unpack: word (r, k) holds columns (r/8)*8*pack + f*8 + r%8, f = 0 in the high bits
+  std::vector<uint8_t> res((size_t)N * K), orig((size_t)N * K);
+  for (int r = 0; r < N / pack; ++r)
+    for (int f = 0; f < pack; ++f) {
+      const size_t n = (size_t)(r / 8) * 8 * pack + f * 8 + r % 8;
+      const int sh = (pack - 1 - f) * w_bits;
+      for (int k = 0; k < K; ++k) res[n * K + k] = (uint8_t)((ref_words[(size_t)r * K + k] >> sh) & mask);
+    }
+  // 2. undo permute_weight: res[idx[x]] = orig[idx[perm[x]]] inside every 16(K) x 8*pack(N) block
+  int perm[32];
+  {
+    const int* proj;
+    const int* desired;
+    int plen;
+    static const int p8[4] = {1, 0, 3, 2}, d8[8] = {0, 2, 4, 6, 1, 3, 5, 7};
+    static const int p4[8] = {3, 7, 2, 6, 1, 5, 0, 4};
+    static const int d4[16] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+    if (w_bits == 8) {
+      proj = p8, desired = d8, plen = 4;
+    } else {
+      proj = p4, desired = d4, plen = 8;
+    }
+    for (int i = 0; i < 4 * pack; i += plen)
+      for (int j = 0; j < plen; ++j) perm[proj[j] + i] = desired[i + j];
+  }
+  for (int j = 0; j < N; j += pack * 8)
+    for (int i = 0; i < K; i += 16)
+      for (int tj = 0; tj < 8; ++tj)
+        for (int ti = 0; ti < 8; ti += 2) {
+          size_t idx[32];
+          int x = 0;
+          for (int ii = 0; ii < 16; ii += 8)
+            for (int tii = 0; tii < 2; ++tii)
+              for (int f = 0; f < pack; ++f) idx[x++] = (size_t)(i + ii + ti + tii) + (size_t)(j + f * 8 + tj) * K;
+          for (int y = 0; y < x; ++y) orig[idx[perm[y]]] = res[idx[y]];
+        }
+  // 3. kernel layout
+  const size_t row_bytes = (size_t)K * w_bits / 8;
+  for (int n = 0; n < N; ++n) {
+    uint8_t* o = out + (size_t)n * row_bytes;
+    if (w_bits == 4) memset(o, 0, row_bytes);
+    for (int k = 0; k < K; ++k) {
+      const int seg = k / 64, kl = k % 64, kc = kl / 32, g = (kl % 32) / 8, e = kl % 8;
+      const size_t pos = (size_t)seg * 64 + g * 16 + kc * 8 + e;
+      const uint8_t u = orig[(size_t)n * K + k];
+      if (w_bits == 8) o[pos] = u;
+      else o[pos / 2] |= (uint8_t)(u << (4 * (pos & 1)));
+    }
+  }
+  return MXMOE_GG_OK;
 }
 
 }  // extern "C"

@@ -31,18 +31,18 @@
 
 namespace mxmoe {
 
-enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_COUNT = 3 };
+enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_COUNT = 5 };
 
 // One row of the plan table (64 B), written by the host planner into the workspace.
 struct GGMeta {
   int32_t M, N, K, qtype;
   int32_t tiles_n;     // cdiv(N, BN of this qtype)
   int32_t tile_begin;  // first global tile id of this problem
-  int32_t kbytes;      // bytes of one K row (K * bits / 8)
-  int32_t reserved;
+  int32_t kbytes;      // bytes of one K row (K * bits / 8; weight-only: of the fp16 A row)
+  int32_t reserved;    // weight-only: 64-K stages per scale group
   int64_t lda_b, ldb_b;  // row strides of A / B in bytes
   int64_t ldc;           // row stride of C in fp16 elements
-  int64_t reserved2;
+  int64_t reserved2;     // weight-only: 1 = sym codes
 };
 static_assert(sizeof(GGMeta) == 64, "GGMeta must stay 64 bytes");
 
@@ -690,31 +690,6 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 }
 
 // v2 fused kernel: qtype x height-class dispatch, uniform per workgroup.
-template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
-__global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
-  const TileDesc td = args.tiles[blockIdx.x];
-  if (td.prob < 0) return;
-  const GGMeta mt = args.meta[td.prob];
-  const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[td.prob]);
-  const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[td.prob]);
-  const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
-  const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
-  _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
-  const bool tall = td.cls == 0;
-  if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  } else if constexpr ((ABL & 7) != 0) {
-    return;  // ablation builds time the int8 path only
-  } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-  }
-}
 
 
 // ============================================================================================
@@ -963,5 +938,217 @@ __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2
 }
 
 
+
+// ============================================================================================
+// Weight-only WxA16 (w4a16 / w8a16, any group size that is a multiple of 64 or per-channel,
+// sym or asym): A fp16, B quantised codes dequantised in registers, fp16 MFMA, f32 accumulate.
+// Reference arithmetic (cta_gemm.cuh:112-286, Converter::dequant_frag quantize.cuh:146-213):
+// b = fp16(fma(u - off, scale, zp)) — one fp16 rounding, as the reference's __hfma2.
+//   * a stage is 64 K ELEMENTS: A as the fp16 v2 path (rows of 128 B, same swizzle and fragment
+//     reads), B rows of 64 * BITS / 8 bytes in the repacked layout of include/mxmoe_gg.h, so one
+//     ds_read_b64 (4-bit) / ds_read_b128 (8-bit) gives a lane its 8 codes of both K halves;
+//   * dequant: v_perm into 0x6400|u (= 1024 + u, exact fp16), v_pk_add_f16 -(1024 + off) (exact),
+//     v_pk_fma_f16 with (scale, scale), (zp, zp);
+//   * scale / zp (reference permute_scale layout [G][N] or [G][N][2]) per lane column, reloaded
+//     when the stage enters a new group.
+// ============================================================================================
+template <int BM_>
+struct WoCfg {
+  static constexpr int BM = BM_, BN = 256, NT = 512, KS = 64;  // KS: K elements per stage
+  static constexpr int WM = 2, WN = 4;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int A_BYTES = BM * 128, B_BYTES_MAX = BN * KS;  // B sized for 8-bit codes
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES_MAX;
+  static constexpr int GA = BM / 64;
+  static_assert(2 * STAGE_BYTES <= V2Cfg<256>::LDS_BYTES, "two stages must fit the v2 LDS image");
+};
+
+__device__ __forceinline__ uint32_t wo_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// 8 codes (K ascending) -> 8 fp16 dequantised values
+template <int BITS>
+__device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uint32_t s2, uint32_t z2) {
+  uint32_t d[4];
+  if constexpr (BITS == 4) {
+    const uint32_t lo = w[0] & 0x0F0F0F0Fu, hi = (w[0] >> 4) & 0x0F0F0F0Fu;  // even / odd K codes
+#pragma unroll
+    for (int q = 0; q < 4; ++q)  // half pair q = (K 2q, K 2q+1): byte q of lo and of hi
+      d[q] = wo_perm(hi, lo, 0x0c040c00u + 0x00010001u * q) | 0x64006400u;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // bytes 2q, 2q+1 of the 8 codes
+      const uint32_t src = w[q >> 1];
+      const uint32_t sel = (q & 1) ? 0x0c030c02u : 0x0c010c00u;
+      d[q] = wo_perm(0, src, sel) | 0x64006400u;
+    }
+  }
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  v8h out;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    h2 x = __builtin_bit_cast(h2, d[q]) + __builtin_bit_cast(h2, moff2);  // exact: u - off
+    x = __builtin_elementwise_fma(x, __builtin_bit_cast(h2, s2), __builtin_bit_cast(h2, z2));
+    out[2 * q] = x[0];
+    out[2 * q + 1] = x[1];
+  }
+  return out;
+}
+
+template <class Cfg, int BITS>
+__device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __restrict__ A,
+                                           const uint8_t* __restrict__ B, const _Float16* __restrict__ SB,
+                                           _Float16* __restrict__ C, int m0, int n0, uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA;
+  constexpr int RB = Cfg::KS * BITS / 8;        // B bytes per row per stage
+  constexpr int LPR = RB / 16, RPI = 64 / LPR;  // lanes per B row, B rows per wave-instruction
+  constexpr int GBW = Cfg::BN / RPI / 8;        // B DMA instructions per wave per stage
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N;
+  const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
+  const int nst = mt.K / Cfg::KS;
+  const int gstages = mt.reserved;  // stages per scale group (>= nst: one group)
+  const bool sym = mt.reserved2 != 0;
+
+  const uint8_t* srcA[GA];
+  const uint8_t* srcB[GBW];
+  {
+    const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int row = (wave * GA + j) * 8 + rsub;
+      srcA[j] = A + (int64_t)min(m0 + row, M - 1) * lda + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < GBW; ++j) {
+      const int row = (wave * GBW + j) * RPI + lane / LPR;
+      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + (lane % LPR) * 16;
+    }
+  }
+  auto issue = [&](int s, int buf) {
+    uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
+    uint8_t* Bs = As + Cfg::A_BYTES;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) glds16(srcA[j] + s * 128, As + (wave * GA + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < GBW; ++j) glds16(srcB[j] + s * RB, Bs + (wave * GBW + j) * 1024);
+  };
+
+  // per-lane columns and their scale / zp pairs (packed (x, x) halves for v_pk_fma_f16)
+  const int ncol0 = n0 + wn * Cfg::WTN;
+  // fp16 -(1024 + off) = 0xE400 | off: sym off = 7 (4-bit) / 127 (8-bit), asym 0
+  const uint32_t moff2 = sym ? (BITS == 4 ? 0xE407E407u : 0xE47FE47Fu) : 0xE400E400u;
+  uint32_t s2[FN], z2[FN];
+  auto load_scales = [&](int grp) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = min(ncol0 + j * 16 + r16, N - 1);
+      if (sym) {
+        const uint32_t s = __builtin_bit_cast(uint16_t, SB[(int64_t)grp * N + n]);
+        s2[j] = s | (s << 16);
+        z2[j] = 0;
+      } else {
+        const uint32_t sz = *reinterpret_cast<const uint32_t*>(SB + ((int64_t)grp * N + n) * 2);
+        s2[j] = (sz & 0xFFFFu) * 0x10001u;
+        z2[j] = (sz >> 16) * 0x10001u;
+      }
+    }
+  };
+
+  v4f acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0, 0, 0, 0};
+
+  const int swz = (r16 >> 1) & 7;
+  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
+  const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * RB;
+  auto compute = [&](int buf) {
+    const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
+    const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
+    uint32_t raw[FN][2];  // 4-bit: the codes of both K halves (one 8-B read); 8-bit: one K half
+    if constexpr (BITS == 4) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + g * 8);
+        raw[j][0] = v.x;
+        raw[j][1] = v.y;
+      }
+    }
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const uint32_t off = (uint32_t)(((kc * 4 + g) ^ swz) << 4);
+      v8h b[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (BITS == 4) {
+          b[j] = wo_dequant<4>(&raw[j][kc], moff2, s2[j], z2[j]);
+        } else {
+          const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + g * 16 + kc * 8);
+          raw[j][0] = v.x;
+          raw[j][1] = v.y;
+          b[j] = wo_dequant<8>(raw[j], moff2, s2[j], z2[j]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const v8h a = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  if (nst > 0) {
+    load_scales(0);
+    issue(0, 0);
+    __syncthreads();
+    for (int s = 0; s < nst; ++s) {
+      if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
+      if (s > 0 && s % gstages == 0) load_scales(s / gstages);
+      compute(s & 1);
+      __syncthreads();
+    }
+  }
+  epilogue_v3<Cfg, QT_F16>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
+}
+
+template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
+__global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
+  const TileDesc td = args.tiles[blockIdx.x];
+  if (td.prob < 0) return;
+  const GGMeta mt = args.meta[td.prob];
+  const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[td.prob]);
+  const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[td.prob]);
+  const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
+  const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
+  _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
+  const bool tall = td.cls == 0;
+  if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if constexpr ((ABL & 7) != 0) {
+    return;  // ablation builds time the int8 path only
+  } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
+    if (tall) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
+    if (tall) gg_tile_wo<WoCfg<256>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    else gg_tile_wo<WoCfg<128>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
+  } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
+    if (tall) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    else gg_tile_wo<WoCfg<128>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
+  }
+}
 
 }  // namespace mxmoe

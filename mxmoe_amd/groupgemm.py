@@ -36,6 +36,11 @@ class QParams:
         return self.a_bits < 16 or self.w_bits < 16
 
     @property
+    def is_weight_only(self) -> bool:
+        """WxA16: fp16 A, quantised B (scale / zp per column or group), cta_gemm.cuh:112-421."""
+        return self.a_bits == 16 and self.w_bits < 16
+
+    @property
     def qcfg(self) -> str:
         if not self.is_quant:
             return "fp16"
@@ -54,8 +59,15 @@ class QParams:
 FP16 = QParams()
 W8A8 = QParams(8, 8, -1, True)
 W4A4 = QParams(4, 4, -1, True)
+# weight-only (any group size that is -1 or a multiple of 64 dividing K, sym or asym, 4 / 8 bits)
+W4A16_G128_ASYM = QParams(16, 4, 128, False)
+W4A16_ASYM = QParams(16, 4, -1, False)
+W4A16_G128_SYM = QParams(16, 4, 128, True)
+W8A16_ASYM = QParams(16, 8, -1, False)
 
-SUPPORTED = {FP16.qcfg: FP16, W8A8.qcfg: W8A8, W4A4.qcfg: W4A4}
+SUPPORTED = {q.qcfg: q for q in (FP16, W8A8, W4A4, W4A16_G128_ASYM, W4A16_ASYM, W4A16_G128_SYM, W8A16_ASYM,
+                                  QParams(16, 4, -1, True), QParams(16, 8, -1, True), QParams(16, 8, 128, True),
+                                  QParams(16, 8, 128, False))}
 
 
 @dataclasses.dataclass

@@ -21,7 +21,7 @@ from typing import Optional, Sequence
 import torch
 
 from .groupgemm import GroupGemm, Problem, QParams
-from .quantize import pack_wxax, quant_rtn_sym
+from .quantize import pack_weightonly_mi355x, pack_wxax, quant_rtn_sym, quant_weightonly
 from .workload import QShape
 
 
@@ -58,7 +58,12 @@ def build_layer_inputs(shapes: Sequence[QShape], device="cuda", seed: int = 42,
         a = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).to(torch.float16)
         b = (torch.rand(N, K, generator=g, device=dev) * 2 - 1).to(torch.float16)
         C = torch.empty(max(M, 1), N, dtype=torch.float16, device=dev)
-        if q.is_quant:
+        if q.is_weight_only:
+            codes, sz = quant_weightonly(b, q.w_bits, q.gsize, q.sym)
+            probs.append(Problem(A=a, B=pack_weightonly_mi355x(codes, q.w_bits), C=C, M=M, N=N, K=K, q=q,
+                                 scale_b=sz))
+            del codes
+        elif q.is_quant:
             qa, sa = quant_rtn_sym(a, q.a_bits)
             qb, sb = quant_rtn_sym(b, q.w_bits)
             A, B = pack_wxax(qa, q.a_bits), pack_wxax(qb, q.w_bits)

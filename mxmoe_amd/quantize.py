@@ -1,5 +1,13 @@
 """Input preparation for quantised GroupGEMM problems (bench / test setup — not the hot path).
 
+Weight-only (WxA16) inputs: ``quant_weightonly`` restates the reference's ``quant_weight``
+(quantize.cuh:218-279) per (column, group) in fp16 (sym: scale = max|w| / qmax, zp = 0;
+asym: zp = min, scale = (max - min) / (2^bits - 1)), returning the codes as ``pack_weightonly``
+stores them (sym offset by 2^(bits-1) - 1) and scale / zp in the reference ``permute_scale``
+layout; ``pack_weightonly_mi355x`` writes the kernel layout documented at
+``mxmoe_gg_repack_weightonly`` (include/mxmoe_gg.h). Reference-packed weights go through
+``_native.repack_weightonly`` instead.
+
 Restates, in torch (runs on CPU or on the GPU for the bs=8192 shapes):
   * ``quant_rtn_sym``: RTN per-row symmetric quantisation in fp16, the reference's
     ``quant_weight`` kernel (mxmoe/kernels/src/include/quantize.cuh:218-279) and
@@ -71,3 +79,46 @@ def quantize_pack(x: torch.Tensor, bits: int) -> tuple[torch.Tensor, torch.Tenso
     """fp16 [rows, K] -> (packed uint8, fp16 scale, int8 codes)."""
     q, s = quant_rtn_sym(x, bits)
     return pack_wxax(q, bits), s, q
+
+
+def quant_weightonly(w: torch.Tensor, bits: int, gsize: int, sym: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp16 [N, K] -> (stored codes uint8 [N, K], scale_zp fp16 flat: sym [G][N], asym [G][N][2])."""
+    if w.dtype != torch.float16:
+        raise TypeError("quant_weightonly expects fp16 input (the reference quantises in half)")
+    if bits not in (4, 8):
+        raise ValueError("weight-only: 4 / 8-bit codes")
+    N, K = w.shape
+    g = K if gsize == -1 else gsize
+    if K % g:
+        raise ValueError("K must be a multiple of the group size")
+    grp = w.reshape(N, K // g, g)
+    lo, hi = grp.amin(dim=-1), grp.amax(dim=-1)
+    if sym:
+        qmax = (1 << (bits - 1)) - 1
+        lower, upper = -qmax, qmax
+        zp = torch.zeros_like(lo)
+        scale = torch.maximum(lo.abs(), hi.abs()) / upper
+    else:
+        lower, upper = 0, (1 << bits) - 1
+        zp = lo
+        scale = (hi - lo) / upper
+    scale = torch.where(scale == 0, torch.ones_like(scale), scale)
+    q = ((grp - zp[..., None]) / scale[..., None]).clamp(lower, upper).round()  # half-to-even
+    codes = (q.to(torch.int16) + ((1 << (bits - 1)) - 1 if sym else 0)).to(torch.uint8).reshape(N, K)
+    if sym:
+        sz = scale.t().contiguous().reshape(-1)
+    else:
+        sz = torch.stack([scale, zp], dim=-1).transpose(0, 1).contiguous().reshape(-1)
+    return codes, sz
+
+
+def pack_weightonly_mi355x(codes: torch.Tensor, bits: int) -> torch.Tensor:
+    """Stored codes uint8 [N, K] -> kernel layout uint8 [N, K * bits / 8]: in each 64-K segment the
+    K values {kc*32 + g*8 + e} sit at element position g*16 + kc*8 + e; 4-bit low nibble first."""
+    N, K = codes.shape
+    if K % 64:
+        raise ValueError("weight-only needs K % 64 == 0")
+    u = codes.reshape(N, K // 64, 2, 4, 8).transpose(2, 3).reshape(N, K)
+    if bits == 8:
+        return u.contiguous()
+    return (u[:, 0::2] | (u[:, 1::2] << 4)).contiguous()

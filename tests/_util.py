@@ -4,9 +4,10 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from mxmoe_amd import _native as nat
 from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, Problem, QParams
 from mxmoe_amd.quantize import pack_wxax, quant_rtn_sym
-from oracle import oracle
+from oracle import oracle, weightonly
 
 QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4}
 
@@ -15,12 +16,24 @@ class HostProblem:
     """Host copies of one problem's inputs (numpy) + the device Problem."""
 
     def __init__(self, M, N, K, q: QParams, seed: int, device: str, ldc: int = 0, C: torch.Tensor | None = None,
-                 c_col0: int = 0):
+                 c_col0: int = 0, ref_format: bool = False):
         g = torch.Generator().manual_seed(seed)
         self.M, self.N, self.K, self.q = M, N, K, q
         a = (torch.rand(M, K, generator=g, dtype=torch.float32) * 2 - 1).to(torch.float16)
         b = (torch.rand(N, K, generator=g, dtype=torch.float32) * 2 - 1).to(torch.float16)
-        if q.is_quant:
+        if q.is_weight_only:
+            # oracle quantisation; B either packed straight into the kernel layout or built in the
+            # reference's packed format and converted by the library (the drop-in route)
+            qv, sz = weightonly.quant_wo(b.numpy(), q.w_bits, q.gsize, q.sym)
+            self.sb = weightonly.permute_scale(sz, N, K, q.gsize, q.sym)
+            self.qb = qv
+            if ref_format:
+                self.B = nat.repack_weightonly(weightonly.ref_pack(qv, q.w_bits, q.sym), N, K, q.w_bits)
+            else:
+                self.B = weightonly.mi355x_pack(qv, q.w_bits, q.sym)
+            self.A = a.numpy()
+            self.sa = None
+        elif q.is_quant:
             bits = q.a_bits
             qa, sa = quant_rtn_sym(a, bits)
             qb, sb = quant_rtn_sym(b, bits)
@@ -47,6 +60,9 @@ class HostProblem:
             ldc=self.ldc if C is None else C.shape[1])
 
     def expected(self) -> np.ndarray:
+        if self.q.is_weight_only:
+            q = self.q
+            return weightonly.gemm(self.A, weightonly.dequant(self.qb, self.sb, self.N, self.K, q.w_bits, q.gsize, q.sym))
         if self.q.is_quant:
             return oracle.gg_quant(self.A, self.B, self.sa, self.sb, self.M, self.N, self.K, self.q.a_bits)
         return oracle.gg_f16(self.A, self.B, self.M, self.N, self.K)
