@@ -40,6 +40,13 @@ CONFIGS = {
                   name="qwen2_moe layer-11 mixed w4a4+w8a8 (wbits=5.0, LP-1 qconfig) bs=8192"),
     "ds2_mixed": dict(kw="ds2_mixed", peak="int8", dtype="int4+int8",
                       name="DeepSeek-V2-Lite MoE layer mixed w4a4+w8a8 (25 % w8a8 units) bs=8192, 64 experts"),
+    # weight-only: fp16 activations, int4 weights dequantised to fp16 MFMA
+    "w4a16": dict(kw=dict(qstr="w4a16_g128_asym"), peak="fp16", dtype="fp16 (int4 weights)",
+                  name="qwen2_moe layer-11 w4a16_g128_asym GroupGEMM bs=8192"),
+    "w4a16_bs512": dict(kw=dict(qstr="w4a16_g128_asym"), peak="fp16", dtype="fp16 (int4 weights)", bs=512,
+                        name="qwen2_moe layer-11 w4a16_g128_asym GroupGEMM bs=512 (weight-bandwidth bound)"),
+    "fp16_bs512": dict(kw={}, peak="fp16", dtype="fp16", bs=512,
+                       name="qwen2_moe layer-11 fp16 GroupGEMM bs=512"),
 }
 
 
@@ -59,6 +66,7 @@ def full_layer(cfg: str, bs: int = 8192):
     from mxmoe_amd.workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1,
                                     qwen2_layer11_workload)
 
+    bs = CONFIGS[cfg].get("bs", bs)
     kw = CONFIGS[cfg]["kw"]
     if kw == "ds2_mixed":
         return load_workload(ds2_workload(bs, qconfig=ds2_mixed_qconfig()))["layer-1"]
@@ -279,6 +287,16 @@ def main():
     f_gu, f_dn = main_res["flops"]["gate_up"], main_res["flops"]["down"]
     t_gu, t_dn = per["gate_up"]["mean_ms"], per["down"]["mean_ms"]
     achieved = (f_gu + f_dn) / ((t_gu + t_dn) * 1e-3) / 1e12
+    # roofline of the step's two launches: MFMA-bound unless the arithmetic intensity puts the
+    # HBM roof (algorithmic bytes x 8 TB/s) below the MFMA peak (small batches, weight-only)
+    b_step = main_res["bytes"]["gate_up"] + main_res["bytes"]["down"]
+    if (f_gu + f_dn) / b_step * HBM_GBS / 1e3 < peak:
+        gbs = b_step / ((t_gu + t_dn) * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_GBS, "unit": "GB/s", "frac": round(gbs / HBM_GBS, 4),
+                "achieved_tflops": round(achieved, 2)}
+    else:
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4)}
     value = main_res["total_flops"] * args.steps / main_res["dt"] / 1e12
     pmc = load_pmc_traffic(cfg) if world == 1 else None  # the committed PMC passes are single-GPU runs
 
@@ -357,12 +375,11 @@ def main():
                                                          "seeded multinomial (SURVEY.md 8d)"),
             "config": {"workload": CONFIGS[cfg]["name"] + (f", expert-parallel over {world} GPUs" if world > 1 else ""),
                        "model": ("DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")
-                       + " MoE GroupGEMMs", "global_batch": 8192 * world,
+                       + " MoE GroupGEMMs", "global_batch": CONFIGS[cfg].get("bs", 8192) * world,
                        "seq_len": None, "parallelism": f"ep{world}" if world > 1 else "single",
                        "problems_per_call": len(main_res["shapes"]["gate_up"]), "variant": main_res["variant"],
                        "variant_name": nat.list_variants()[main_res["variant"]].split()[1]},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4),
+            "roofline": {**roof,
                          "traffic": pmc.get("hbm_bytes_per_step") if isinstance(pmc, dict) else None,
                          "kernel": kernel_symbol(nat.list_variants()[main_res["variant"]].split()[1])
                          + " (gate_up + down launches; achieved = sum FLOPs / sum mean launch time)",

@@ -59,6 +59,7 @@ struct Variant {
   int chunk;           // tiles per XCD chunk (workgroups that run together on one XCD)
   int k_stage_bytes;   // K bytes per row must be a multiple of this (0 = any multiple of 16)
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
+  int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
   void (*launch)(const GGArgs&, int grid, int qmask, hipStream_t);  // qmask: 1 << QType present
 };
 
@@ -84,7 +85,9 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       case 7: launch_v2_q<ABL, 7>(a, grid, s); break;
       case 8: launch_v2_q<ABL, 8>(a, grid, s); break;    // w4a16 only
       case 16: launch_v2_q<ABL, 16>(a, grid, s); break;  // w8a16 only
-      default: launch_v2_q<ABL, 31>(a, grid, s); break;
+      // any other mix: every tile body in one kernel. The staggered int bodies leave no register
+      // room for that (the compiler spilled inside their K loops), so the fallback is plain v2.
+      default: launch_v2_q<0, 31>(a, grid, s); break;
     }
   }
 }
@@ -153,6 +156,7 @@ Variant make_v2(const char* name) {
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
   v.k_stage_bytes = 0;  // K tails handled in-kernel (last stage)
   v.tail_bm = 128;
+  v.tail2_bm = 64;  // <= 64 remaining rows, fp16 / weight-only problems (small batches)
   v.launch = &launch_v2<ABL>;
   return v;
 }
@@ -332,7 +336,7 @@ struct Plan {
 
 // Tile generation + scheduling.
 //  1. per problem: m-tiles of the variant's height (v2: 256-row tiles while > tail_bm rows remain,
-//     then one tail_bm tile), n-tiles of width bn; tiles enumerated in 4-m-tile bands, n-major
+//     then one tail_bm (128) or tail2_bm (64) tile), n-tiles of width bn; 4-m-tile bands, n-major
 //     inside a band, so 32 consecutive tiles form a ~4 x 8 block sharing A rows and B columns;
 //  2. problems by descending per-tile cost (K bytes x tile area x MFMA passes), longest first;
 //  3. the sequence is cut into chunks of `chunk` tiles; chunk c runs on XCD c % 8 in round c / 8:
@@ -365,7 +369,11 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     std::vector<std::pair<int, int>> mt;  // (m0, cls)
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
-      if (v.kind != Kind::V0 && v.tail_bm && rem <= v.tail_bm) {
+      const bool small_class = m.qtype == QT_F16 || m.qtype == QT_W4A16 || m.qtype == QT_W8A16;
+      if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
+        mt.push_back({m0, 2});
+        m0 += v.tail2_bm;
+      } else if (v.kind != Kind::V0 && v.tail_bm && rem <= v.tail_bm) {
         mt.push_back({m0, 1});
         m0 += v.tail_bm;
       } else {

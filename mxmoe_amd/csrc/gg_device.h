@@ -952,15 +952,27 @@ __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2
 //   * scale / zp (reference permute_scale layout [G][N] or [G][N][2]) per lane column, reloaded
 //     when the stage enters a new group.
 // ============================================================================================
-template <int BM_>
+// WM_ = waves along M: 2 for 256-row tiles; 1 for the 128 / 64-row classes, so that each B
+// fragment is dequantised by exactly one wave and reused over all its 4-8 A fragments (with 2 x 4
+// waves and 32-row wave tiles the dequant VALU outweighed the MFMAs 11:1 at small batch)
+template <int BM_, int WM_ = 2>
 struct WoCfg {
   static constexpr int BM = BM_, BN = 256, NT = 512, KS = 64;  // KS: K elements per stage
-  static constexpr int WM = 2, WN = 4;
+  static constexpr int WM = WM_, WN = 8 / WM_;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
   static constexpr int A_BYTES = BM * 128, B_BYTES_MAX = BN * KS;  // B sized for 8-bit codes
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES_MAX;
   static constexpr int GA = BM / 64;
+  // LDS ring: as many stages as the kernel's 128-KiB image holds (2 at 256 rows, 4 at 128, 8 at 64
+  // rows with 4-bit codes), all but one in flight — small tiles have little MFMA work per stage, so
+  // they need the deeper prefetch to cover the load latency
+  template <int BITS>
+  static constexpr int stage_bytes() { return A_BYTES + BN * KS * BITS / 8; }
+  template <int BITS>
+  static constexpr int nbuf() {
+    return V2Cfg<256>::LDS_BYTES / stage_bytes<BITS>() > 8 ? 8 : V2Cfg<256>::LDS_BYTES / stage_bytes<BITS>();
+  }
   static_assert(2 * STAGE_BYTES <= V2Cfg<256>::LDS_BYTES, "two stages must fit the v2 LDS image");
 };
 
@@ -1004,7 +1016,12 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA;
   constexpr int RB = Cfg::KS * BITS / 8;        // B bytes per row per stage
   constexpr int LPR = RB / 16, RPI = 64 / LPR;  // lanes per B row, B rows per wave-instruction
+  // B chunk swizzle: the 16-B chunk c of tile row n sits in LDS slot c ^ ((n >> RSH) & (LPR - 1)),
+  // RSH = log2(rows per 256-B bank window); rows n, n + 256 / RB then hit different banks
+  constexpr int RSH = BITS == 4 ? 3 : 2;
   constexpr int GBW = Cfg::BN / RPI / 8;        // B DMA instructions per wave per stage
+  constexpr int SB_ = Cfg::template stage_bytes<BITS>(), NBUF = Cfg::template nbuf<BITS>(), DIST = NBUF - 1;
+  constexpr int DPS = GA + GBW;  // LDS-DMA instructions per wave per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
@@ -1027,11 +1044,12 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
     for (int j = 0; j < GBW; ++j) {
       const int row = (wave * GBW + j) * RPI + lane / LPR;
-      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + (lane % LPR) * 16;
+      const int chunk = (lane % LPR) ^ ((row >> RSH) & (LPR - 1));  // source chunk for this LDS slot
+      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + chunk * 16;
     }
   }
   auto issue = [&](int s, int buf) {
-    uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
+    uint8_t* As = lds + buf * SB_;
     uint8_t* Bs = As + Cfg::A_BYTES;
 #pragma unroll
     for (int j = 0; j < GA; ++j) glds16(srcA[j] + s * 128, As + (wave * GA + j) * 1024);
@@ -1043,19 +1061,19 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const int ncol0 = n0 + wn * Cfg::WTN;
   // fp16 -(1024 + off) = 0xE400 | off: sym off = 7 (4-bit) / 127 (8-bit), asym 0
   const uint32_t moff2 = sym ? (BITS == 4 ? 0xE407E407u : 0xE47FE47Fu) : 0xE400E400u;
-  uint32_t s2[FN], z2[FN];
-  auto load_scales = [&](int grp) {
+  uint32_t s2[FN], z2[FN], s2n[FN], z2n[FN];  // current group, next group (prefetched)
+  auto load_scales = [&](int grp, uint32_t (&so)[FN], uint32_t (&zo)[FN]) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = min(ncol0 + j * 16 + r16, N - 1);
       if (sym) {
         const uint32_t s = __builtin_bit_cast(uint16_t, SB[(int64_t)grp * N + n]);
-        s2[j] = s | (s << 16);
-        z2[j] = 0;
+        so[j] = s | (s << 16);
+        zo[j] = 0;
       } else {
         const uint32_t sz = *reinterpret_cast<const uint32_t*>(SB + ((int64_t)grp * N + n) * 2);
-        s2[j] = (sz & 0xFFFFu) * 0x10001u;
-        z2[j] = (sz >> 16) * 0x10001u;
+        so[j] = (sz & 0xFFFFu) * 0x10001u;
+        zo[j] = (sz >> 16) * 0x10001u;
       }
     }
   };
@@ -1069,14 +1087,16 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const int swz = (r16 >> 1) & 7;
   const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * RB;
+  // rows of a B fragment are base + r16 with base % 16 == 0, so the swizzle depends on r16 only
+  const int bsw = (r16 >> RSH) & (LPR - 1);
   auto compute = [&](int buf) {
-    const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
-    const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
+    const uint8_t* As = lds + buf * SB_ + a_row;
+    const uint8_t* Bs = lds + buf * SB_ + Cfg::A_BYTES + b_row;
     uint32_t raw[FN][2];  // 4-bit: the codes of both K halves (one 8-B read); 8-bit: one K half
     if constexpr (BITS == 4) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + g * 8);
+        const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + (((g >> 1) ^ bsw) << 4) + (g & 1) * 8);
         raw[j][0] = v.x;
         raw[j][1] = v.y;
       }
@@ -1090,7 +1110,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
         if constexpr (BITS == 4) {
           b[j] = wo_dequant<4>(&raw[j][kc], moff2, s2[j], z2[j]);
         } else {
-          const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + g * 16 + kc * 8);
+          const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + ((g ^ bsw) << 4) + kc * 8);
           raw[j][0] = v.x;
           raw[j][1] = v.y;
           b[j] = wo_dequant<8>(raw[j], moff2, s2[j], z2[j]);
@@ -1105,16 +1125,42 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     }
   };
 
+  // wait until stage t's LDS-DMA (this wave's) has landed, `later` stages having been issued after it
+  auto wait_stage = [&](int later) {
+    if constexpr (DIST >= 7) if (later >= 6) { wait_vmcnt<6 * DPS>(); return; }
+    if constexpr (DIST >= 6) if (later == 5) { wait_vmcnt<5 * DPS>(); return; }
+    if constexpr (DIST >= 5) if (later == 4) { wait_vmcnt<4 * DPS>(); return; }
+    if constexpr (DIST >= 4) if (later == 3) { wait_vmcnt<3 * DPS>(); return; }
+    if constexpr (DIST >= 3) if (later == 2) { wait_vmcnt<2 * DPS>(); return; }
+    if constexpr (DIST >= 2) if (later == 1) { wait_vmcnt<DPS>(); return; }
+    wait_vmcnt<0>();
+  };
   if (nst > 0) {
-    load_scales(0);
-    issue(0, 0);
-    __syncthreads();
+    load_scales(0, s2, z2);
+#pragma unroll
+    for (int p = 0; p < DIST; ++p)
+      if (p < nst) issue(p, p);
     for (int s = 0; s < nst; ++s) {
-      if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
-      if (s > 0 && s % gstages == 0) load_scales(s / gstages);
-      compute(s & 1);
-      __syncthreads();
+      // stages s+1 .. min(s+DIST-1, nst-1) were issued after s (younger scale loads only make the
+      // in-order count wait longer, never shorter)
+      wait_stage(min(DIST - 1, nst - 1 - s));
+      lds_barrier();  // stage s visible to every wave; buffer (s-1) % NBUF released by all
+      // next group's scales BEFORE this iteration's DMA: the wait the compiler places before their
+      // use then leaves the (younger) DMA in flight instead of draining it
+      const bool next_group = (s + 1) % gstages == 0 && s + 1 < nst;
+      if (next_group) load_scales((s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
+      if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
+      compute(s % NBUF);
+      if (next_group) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          s2[j] = s2n[j];
+          z2[j] = z2n[j];
+        }
+      }
     }
+    wait_vmcnt<0>();
+    lds_barrier();  // ring -> epilogue staging
   }
   epilogue_v3<Cfg, QT_F16>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
 }
@@ -1130,24 +1176,29 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
   const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
-  const bool tall = td.cls == 0;
+  // 0: 256 rows, 1: 128, 2: 64 (fp16 / weight-only only: the int bodies sit at the 256-VGPR edge
+  // and a third inlined height made the compiler spill inside their K loops)
+  const int cls = td.cls;
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);  // no 64-row class
   } else if constexpr ((ABL & 7) != 0) {
     return;  // ablation builds time the int8 path only
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);  // no 64-row class
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
-    if (tall) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v2<V2Cfg<64>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
-    if (tall) gg_tile_wo<WoCfg<256>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
-    else gg_tile_wo<WoCfg<128>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    else gg_tile_wo<WoCfg<64, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
   } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
-    if (tall) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
-    else gg_tile_wo<WoCfg<128>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    else gg_tile_wo<WoCfg<64, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
   }
 }
 

@@ -41,7 +41,9 @@ class LayerInputs:
             ab = 16 if s.qcfg == "fp16" else s.a_bits
             wb = 16 if s.qcfg == "fp16" else s.w_bits
             tot += (s.M * s.K * ab + s.N * s.K * wb) // 8 + 2 * s.M * s.N
-            if s.qcfg != "fp16":
+            if s.qcfg != "fp16" and ab == 16:  # weight-only: scale (+ zp) per column and group
+                tot += 2 * s.N * (1 if s.gsize == -1 else s.K // s.gsize) * (1 if s.sym else 2)
+            elif s.qcfg != "fp16":
                 tot += 2 * (s.M + s.N)
         return tot
 

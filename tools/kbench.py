@@ -30,11 +30,14 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="all", choices=["all", "shared", "routed"])
     ap.add_argument("--rounds", type=int, default=5, help="round-robin rounds over the variants")
+    ap.add_argument("--bs", type=int, default=8192, help="tokens (routed M_e scale with it)")
     ap.add_argument("--settle-s", type=float, default=1.0, help="seconds of load before timing")
     args = ap.parse_args()
     kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
-          "mixed": dict(qconfig=mixed_qconfig_lp1())}[args.cfg]
-    shapes = load_workload(qwen2_layer11_workload(8192, **kw))["layer-11"][args.gg]
+          "mixed": dict(qconfig=mixed_qconfig_lp1()), "w4a16": dict(qstr="w4a16_g128_asym"),
+          "w4a16c": dict(qstr="w4a16_g-1_sym"), "w8a16": dict(qstr="w8a16_g-1_asym"),
+          "w4a16ga": dict(qstr="w4a16_g-1_asym"), "w4a16gs": dict(qstr="w4a16_g128_sym")}[args.cfg]
+    shapes = load_workload(qwen2_layer11_workload(args.bs, **kw))["layer-11"][args.gg]
     if args.only == "shared":
         shapes = shapes[-1:]
     elif args.only == "routed":
@@ -60,7 +63,8 @@ def main():
         print(json.dumps({"variant": gg.variant, "cfg": args.cfg, "gg": args.gg, "only": args.only,
                           "median_ms": round(med, 4), "spread_ms": round(max(ts) - min(ts), 4),
                           "tiles": gg.total_tiles, "grid": gg.info.grid,
-                          "tflops": round(inp.flops / (med * 1e-3) / 1e12, 1)}), flush=True)
+                          "tflops": round(inp.flops / (med * 1e-3) / 1e12, 1),
+                          "gbs": round(inp.bytes_algorithmic() / (med * 1e-3) / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":
