@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MXMOE_GG_ABI_VERSION 2
+#define MXMOE_GG_ABI_VERSION 3
 
 enum {
   MXMOE_GG_OK = 0,
@@ -84,7 +84,7 @@ typedef struct mxmoe_gg_plan_info {
   int32_t lds_bytes;
   int32_t qtype_mask;      /* bit q set if a planned problem has quant type q (0 fp16, 1 w8a8, 2 w4a4);
                             * selects the kernel specialisation at launch */
-  int32_t reserved_;
+  int32_t splitk_slabs;    /* 256-KiB partial-sum slabs the plan's split-K tiles use (0: no split) */
   int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */
   void* workspace;         /* device workspace the plan was written to */
 } mxmoe_gg_plan_info;

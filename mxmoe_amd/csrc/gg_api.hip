@@ -187,9 +187,11 @@ const std::vector<Variant>& variants() {
 }
 
 // AUTO policy (profiles/r01/kbench_*.jsonl, qwen2_moe layer 11): the staggered 256x256 v2 is the
-// fastest whenever fp16 or w8a8 problems are present; int4-only sets run 256x128 tiles, 2 WG/CU.
+// fastest whenever fp16 or w8a8 problems are present; int4-only sets run 256x128 tiles, 2 WG/CU,
+// unless they are low-fill enough to need split-K (v2 kernels only).
 constexpr const char* kDefaultVariantName = "v2s_256x256_w8_dma_stagger";
 constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
+constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
   for (size_t i = 0; i < variants().size(); ++i)
@@ -228,15 +230,19 @@ struct HostProblem {
 };
 
 // Workspace: [GGMeta x P][ptr_A x P][ptr_B x P][ptr_SA x P][ptr_SB x P][ptr_C x P][TileDesc x grid]
+// workspace: plan table | 5 pointer columns | tile table | split-K counters (one per tile slot,
+// zero between launches) | split-K slabs
 struct WsLayout {
-  size_t meta, ptr, tiles, total;
+  size_t meta, ptr, tiles, counters, slabs, total;
 };
-WsLayout ws_layout(int P, int grid) {
+WsLayout ws_layout(int P, int grid, int slabs) {
   WsLayout l;
   l.meta = align_up((size_t)std::max(P, 1) * sizeof(GGMeta), 256);
   l.ptr = align_up((size_t)std::max(P, 1) * sizeof(void*), 256);
   l.tiles = align_up((size_t)std::max(grid, 1) * sizeof(TileDesc), 256);
-  l.total = l.meta + 5 * l.ptr + l.tiles;
+  l.counters = slabs ? align_up((size_t)grid * sizeof(int32_t), 256) : 0;
+  l.slabs = (size_t)slabs * SPLITK_SLAB_BYTES;
+  l.total = l.meta + 5 * l.ptr + l.tiles + l.counters + l.slabs;
   return l;
 }
 
@@ -332,6 +338,7 @@ struct Plan {
   std::vector<int> order;       // table row -> caller's problem index
   std::vector<TileDesc> tiles;  // indexed by blockIdx
   int total_tiles = 0;
+  int slabs = 0;                // split-K partial slabs
 };
 
 // Tile generation + scheduling.
@@ -353,20 +360,21 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   std::vector<int> order;
   for (int i = 0; i < P; ++i)
     if (probs[i].M > 0 && probs[i].N > 0) order.push_back(i);
-  auto tile_cost = [&](int i) {
+  // K stages of a problem in its tile body (v2: 128 B per stage; weight-only: 64 elements)
+  auto stages_of = [&](const GGMeta& m) {
+    if (m.qtype == QT_W4A16 || m.qtype == QT_W8A16) return m.K / 64;
+    return (m.kbytes + v.geom[m.qtype].bkb - 1) / v.geom[m.qtype].bkb;
+  };
+  auto full_tile_cost = [&](int i) {
     const GGMeta& m = all[i];
     const double passes = m.qtype == QT_I4 ? 2.0 : 1.0;  // int4: 2 MFMA passes per staged byte
     return passes * (double)m.kbytes * v.geom[m.qtype].bm * v.geom[m.qtype].bn;
   };
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost(a) > tile_cost(b); });
-
-  plan->meta.clear();
-  plan->order = order;
-  std::vector<TileDesc> seq;
-  for (int row = 0; row < (int)order.size(); ++row) {
-    GGMeta m = all[order[row]];
+  // m-tiles of a problem: (m0, class); v2 classes 256 / 128 / 64 rows (see Variant::tail_bm)
+  auto class_rows = [&](int cls, const TileGeom& g) { return cls == 0 ? g.bm : cls == 1 ? v.tail_bm : v.tail2_bm; };
+  auto m_tiles = [&](const GGMeta& m) {
     const TileGeom& g = v.geom[m.qtype];
-    std::vector<std::pair<int, int>> mt;  // (m0, cls)
+    std::vector<std::pair<int, int>> mt;
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
       const bool small_class = m.qtype == QT_F16 || m.qtype == QT_W4A16 || m.qtype == QT_W8A16;
@@ -381,12 +389,58 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
         m0 += g.bm;
       }
     }
+    return mt;
+  };
+  // split-K (v2 kernels): a problem whose largest tile is far longer than one CU's share of the
+  // whole call (low-fill calls: small batches, long-K shared experts, per-rank work lists) has its
+  // tiles cut into split[i] K slices of >= 4 stages each, at most 8
+  std::vector<int> split(P, 1);
+  if (v.kind == Kind::V2) {
+    double total = 0;
+    std::vector<double> biggest(P, 0.0);
+    for (int i : order) {
+      const GGMeta& m = all[i];
+      const TileGeom& g = v.geom[m.qtype];
+      const double per_row = full_tile_cost(i) / g.bm;
+      for (const auto& t : m_tiles(m)) {
+        const double c = per_row * class_rows(t.second, g);
+        total += c * m.tiles_n;
+        biggest[i] = std::max(biggest[i], c);
+      }
+    }
+    const double share = total / kSplitCUs;
+    for (int i : order) {
+      const double ratio = biggest[i] / std::max(share, 1.0);
+      if (ratio > 2.0) split[i] = std::max(1, std::min({8, (int)ratio, stages_of(all[i]) / 4}));
+    }
+  }
+  auto tile_cost = [&](int i) { return full_tile_cost(i) / split[i]; };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost(a) > tile_cost(b); });
+
+  plan->meta.clear();
+  plan->order = order;
+  plan->slabs = 0;
+  int groups = 0;
+  std::vector<TileDesc> seq;
+  for (int row = 0; row < (int)order.size(); ++row) {
+    GGMeta m = all[order[row]];
+    const TileGeom& g = v.geom[m.qtype];
+    const std::vector<std::pair<int, int>> mt = m_tiles(m);  // (m0, cls)
     m.tile_begin = (int32_t)seq.size();
-    const int nt = m.tiles_n;
+    const int nt = m.tiles_n, S = split[order[row]], nst = stages_of(m);
     for (size_t mb = 0; mb < mt.size(); mb += 4)
       for (int n = 0; n < nt; ++n)
-        for (size_t mi = mb; mi < std::min(mt.size(), mb + 4); ++mi)
-          seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second});
+        for (size_t mi = mb; mi < std::min(mt.size(), mb + 4); ++mi) {
+          if (S == 1) {
+            seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second, 0, nst, -1, -1});
+            continue;
+          }
+          const int grp = groups++, slab = plan->slabs;
+          plan->slabs += S;
+          for (int k = 0; k < S; ++k)  // slices of one tile are consecutive: they start together
+            seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second | (k << 8) | (S << 16),
+                                   k * nst / S, (k + 1) * nst / S, slab, grp});
+        }
     plan->meta.push_back(m);
   }
   const int T = (int)seq.size();
@@ -395,7 +449,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   const int nchunks = (T + chunk - 1) / chunk;
   const int rounds = (nchunks + 7) / 8;
   int grid = 0;
-  plan->tiles.assign((size_t)rounds * 8 * chunk, TileDesc{-1, 0, 0, 0});
+  plan->tiles.assign((size_t)rounds * 8 * chunk, TileDesc{-1, 0, 0, 0, 0, 0, -1, -1});
   for (int s = 0; s < T; ++s) {
     const int c = s / chunk, pos = s % chunk;
     const int b = 8 * (chunk * (c / 8) + pos) + (c % 8);
@@ -424,7 +478,13 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     int qt;
     if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) == MXMOE_GG_OK) mask |= 1 << qt;
   }
-  *out = variant_index(mask == (1 << QT_I4) ? kInt4Variant : kDefaultVariantName);
+  *out = variant_index(kDefaultVariantName);
+  if (mask == (1 << QT_I4)) {
+    // int4-only: the 256x128 2-WG/CU kernel, unless the call is low-fill enough for the v2s plan
+    // to split K (that kernel cannot)
+    Plan p;
+    if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == 0) *out = variant_index(kInt4Variant);
+  }
   return MXMOE_GG_OK;
 }
 
@@ -441,8 +501,8 @@ std::vector<HostProblem> to_host(const mxmoe_gg_problem* problems, int problem_c
 // Host image of the workspace for a plan; pointer columns from `hp` in table-row order.
 std::vector<uint8_t> workspace_image(const Plan& plan, const std::vector<const void*> cols[5], WsLayout* out) {
   const int P = (int)plan.meta.size();
-  const WsLayout l = ws_layout(P, (int)plan.tiles.size());
-  std::vector<uint8_t> img(l.total, 0);
+  const WsLayout l = ws_layout(P, (int)plan.tiles.size(), plan.slabs);
+  std::vector<uint8_t> img(l.total - l.slabs, 0);  // counters start at zero; slabs need no init
   memcpy(img.data(), plan.meta.data(), (size_t)P * sizeof(GGMeta));
   for (int c = 0; c < 5; ++c) memcpy(img.data() + l.meta + c * l.ptr, cols[c].data(), (size_t)P * sizeof(void*));
   memcpy(img.data() + l.meta + 5 * l.ptr, plan.tiles.data(), plan.tiles.size() * sizeof(TileDesc));
@@ -460,7 +520,7 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
   info->lds_bytes = v.lds_bytes;
   info->qtype_mask = 0;
   for (const GGMeta& m : plan.meta) info->qtype_mask |= 1 << m.qtype;
-  info->reserved_ = 0;
+  info->splitk_slabs = plan.slabs;
   info->workspace_bytes = (int64_t)l.total;
   info->workspace = ws;
 }
@@ -531,7 +591,7 @@ int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count,
   Plan plan;
   st = plan_host(hp, variant, false, &plan);
   if (st) return st;
-  *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size()).total;
+  *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size(), plan.slabs).total;
   return MXMOE_GG_OK;
 }
 
@@ -557,7 +617,7 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
   std::vector<uint8_t> img = workspace_image(plan, cols, &l);
   if (!workspace || workspace_bytes < l.total)
     return fail(MXMOE_GG_ERR_WORKSPACE, "workspace too small: need %zu bytes, have %zu", l.total, workspace_bytes);
-  HIP_TRY(hipMemcpyAsync(workspace, img.data(), l.total, hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIP_TRY(hipMemcpyAsync(workspace, img.data(), img.size(), hipMemcpyHostToDevice, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // pageable host image must outlive the copy
   fill_info(plan, variant, l, workspace, info);
   return MXMOE_GG_OK;
@@ -569,7 +629,7 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   if (st) return st;
   if (info->total_tiles == 0) return MXMOE_GG_OK;
   const int P = info->problem_count;
-  const WsLayout l = ws_layout(P, info->grid);
+  const WsLayout l = ws_layout(P, info->grid, info->splitk_slabs);
   const uint8_t* ws = static_cast<const uint8_t*>(info->workspace);
   GGArgs a;
   a.meta = reinterpret_cast<const GGMeta*>(ws);
@@ -581,6 +641,8 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   a.ptr_C = reinterpret_cast<void* const*>(ws + l.meta + 4 * l.ptr);
   a.P = P;
   a.n_slots = info->grid;
+  a.counters = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(ws) + l.meta + 5 * l.ptr + l.tiles);
+  a.slabs = const_cast<uint8_t*>(ws) + l.meta + 5 * l.ptr + l.tiles + l.counters;
   variants()[info->variant].launch(a, info->grid, info->qtype_mask, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return MXMOE_GG_OK;
@@ -643,7 +705,7 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
     HIP_TRY(hipMalloc(&ws, l.total));
     ws_cap = l.total;
   }
-  HIP_TRY(hipMemcpy(ws, img.data(), l.total, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ws, img.data(), img.size(), hipMemcpyHostToDevice));
   mxmoe_gg_plan_info info;
   fill_info(plan, variant, l, ws, &info);
   return mxmoe_gg_launch(&info, nullptr);

@@ -46,14 +46,27 @@ struct GGMeta {
 };
 static_assert(sizeof(GGMeta) == 64, "GGMeta must stay 64 bytes");
 
-// One output tile (16 B), host-built in dispatch order: tile b is run by workgroup b.
+// One output tile (32 B), host-built in dispatch order: tile b is run by workgroup b.
 struct TileDesc {
   int32_t prob;  // row of the plan table; -1 = empty slot (padding of the XCD interleave)
   int32_t m0;    // first output row
   int32_t n0;    // first output column
-  int32_t cls;   // tile-height class (variant specific)
+  int32_t cls;   // bits 0-7 tile-height class; split-K: bits 8-15 slice index, bits 16-23 slices
+  int32_t ks0, ks1;  // K stages [ks0, ks1) of this tile (all of K unless split)
+  int32_t slab;      // split-K: first partial slab of the tile's slices, else -1
+  int32_t grp;       // split-K: arrival counter of the tile, else -1
 };
-static_assert(sizeof(TileDesc) == 16, "TileDesc must stay 16 bytes");
+static_assert(sizeof(TileDesc) == 32, "TileDesc must stay 32 bytes");
+
+// Split-K of one output tile (v2 kernels): slice `idx` of `nsplit` covers K stages
+// [ks0, ks0 + nst); every slice stores its raw accumulators into its slab, the last to arrive
+// sums all slabs in slice order (deterministic; int32 exact) and runs the epilogue.
+constexpr int SPLITK_SLAB_BYTES = 256 * 256 * 4;  // one 256 x 256 tile of 32-bit accumulators
+struct SplitK {
+  int ks0, nst, idx, nsplit, slab, grp;
+  uint8_t* slabs;
+  int32_t* counters;
+};
 
 struct GGArgs {
   const GGMeta* meta;
@@ -65,6 +78,8 @@ struct GGArgs {
   void* const* ptr_C;
   int32_t P;
   int32_t n_slots;  // gridDim.x
+  uint8_t* slabs;     // split-K partial slabs (SPLITK_SLAB_BYTES each)
+  int32_t* counters;  // split-K arrival counters (zero between launches)
 };
 
 typedef int32_t v2i __attribute__((ext_vector_type(2)));
@@ -395,6 +410,54 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Split-K hand-off (cdna_hip_programming.md §6 Guideline 16, counter form): every slice stores
+// its accumulators (thread-linear 16-B words: coalesced), drains, and one lane publishes with an
+// agent-scope release before the relaxed agent-scope ticket; the slice that draws nsplit - 1
+// acquires, re-zeroes the counter for the next launch and sums every slab in slice order.
+// Returns true when `acc` holds the complete K sum (not split, or the last slice).
+template <int NT, class Acc, int FM, int FN>
+__device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& sk, uint8_t* lds) {
+  if (sk.nsplit <= 1) return true;
+  static_assert(FM * FN * NT * 16 <= SPLITK_SLAB_BYTES, "tile accumulators exceed one slab");
+  const int tid = threadIdx.x;
+  Acc* mine = reinterpret_cast<Acc*>(sk.slabs + (size_t)(sk.slab + sk.idx) * SPLITK_SLAB_BYTES);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) mine[(i * FN + j) * NT + tid] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int32_t* flag = reinterpret_cast<int32_t*>(lds);  // the ring is drained: LDS is free here
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(sk.counters + sk.grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == sk.nsplit - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(sk.counters + sk.grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const int last = *flag;
+  __syncthreads();  // every wave has the flag before the epilogue reuses the LDS
+  if (!last) return false;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = Acc{0, 0, 0, 0};
+  for (int k = 0; k < sk.nsplit; ++k) {
+    const Acc* part = reinterpret_cast<const Acc*>(sk.slabs + (size_t)(sk.slab + k) * SPLITK_SLAB_BYTES);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] += part[(i * FN + j) * NT + tid];
+  }
+  return true;
+}
+
 // ABL flags. Timing ablations (results are garbage): 1 = no mainloop DMA (stage 0 reused),
 // 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores.
 // Option (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3.
@@ -459,7 +522,7 @@ template <class Cfg, int QT, int ABL = 0>
 __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
                                            const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
-                                           uint8_t* lds) {
+                                           uint8_t* lds, const SplitK& sk) {
   constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
   typedef typename AccT<QT>::type acc_t;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -468,7 +531,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   const int r16 = lane & 15, g = lane >> 4;
   const int M = mt.M, N = mt.N, kbytes = mt.kbytes;
   const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
-  const int nst = (kbytes + Cfg::BKB - 1) / Cfg::BKB;
+  const int nst = sk.nst, ks0 = sk.ks0;  // this tile's K stages [ks0, ks0 + nst) (all of K unless split)
 
   // per-lane LDS-DMA sources (row clamped, chunk pre-swizzled); + kb per stage
   const uint8_t* srcA[GA];
@@ -494,7 +557,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
     uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
     uint8_t* Bs = As + Cfg::A_BYTES;
-    const int kb = s * Cfg::BKB;
+    const int kb = (ks0 + s) * Cfg::BKB;
     if (kb + Cfg::BKB <= kbytes) {
 #pragma unroll
       for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
@@ -632,6 +695,8 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       __syncthreads();  // own LDS-DMA landed (vmcnt(0)); every wave done reading buffer s&1
     }
   }
+
+  if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
 
   // ---- epilogue: per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
   uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
@@ -1012,7 +1077,7 @@ __device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uin
 template <class Cfg, int BITS>
 __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SB,
-                                           _Float16* __restrict__ C, int m0, int n0, uint8_t* lds) {
+                                           _Float16* __restrict__ C, int m0, int n0, uint8_t* lds, const SplitK& sk) {
   constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA;
   constexpr int RB = Cfg::KS * BITS / 8;        // B bytes per row per stage
   constexpr int LPR = RB / 16, RPI = 64 / LPR;  // lanes per B row, B rows per wave-instruction
@@ -1028,7 +1093,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const int r16 = lane & 15, g = lane >> 4;
   const int M = mt.M, N = mt.N;
   const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
-  const int nst = mt.K / Cfg::KS;
+  const int nst = sk.nst, ks0 = sk.ks0;  // 64-K stages [ks0, ks0 + nst) of this tile
   const int gstages = mt.reserved;  // stages per scale group (>= nst: one group)
   const bool sym = mt.reserved2 != 0;
 
@@ -1052,9 +1117,9 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     uint8_t* As = lds + buf * SB_;
     uint8_t* Bs = As + Cfg::A_BYTES;
 #pragma unroll
-    for (int j = 0; j < GA; ++j) glds16(srcA[j] + s * 128, As + (wave * GA + j) * 1024);
+    for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < GBW; ++j) glds16(srcB[j] + s * RB, Bs + (wave * GBW + j) * 1024);
+    for (int j = 0; j < GBW; ++j) glds16(srcB[j] + (ks0 + s) * RB, Bs + (wave * GBW + j) * 1024);
   };
 
   // per-lane columns and their scale / zp pairs (packed (x, x) halves for v_pk_fma_f16)
@@ -1136,7 +1201,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     wait_vmcnt<0>();
   };
   if (nst > 0) {
-    load_scales(0, s2, z2);
+    load_scales(ks0 / gstages, s2, z2);
 #pragma unroll
     for (int p = 0; p < DIST; ++p)
       if (p < nst) issue(p, p);
@@ -1147,8 +1212,8 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       lds_barrier();  // stage s visible to every wave; buffer (s-1) % NBUF released by all
       // next group's scales BEFORE this iteration's DMA: the wait the compiler places before their
       // use then leaves the (younger) DMA in flight instead of draining it
-      const bool next_group = (s + 1) % gstages == 0 && s + 1 < nst;
-      if (next_group) load_scales((s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
+      const bool next_group = (ks0 + s + 1) % gstages == 0 && s + 1 < nst;
+      if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
       if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
       compute(s % NBUF);
       if (next_group) {
@@ -1162,6 +1227,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     wait_vmcnt<0>();
     lds_barrier();  // ring -> epilogue staging
   }
+  if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
   epilogue_v3<Cfg, QT_F16>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
 }
 
@@ -1178,27 +1244,36 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
   // 0: 256 rows, 1: 128, 2: 64 (fp16 / weight-only only: the int bodies sit at the 256-VGPR edge
   // and a third inlined height made the compiler spill inside their K loops)
-  const int cls = td.cls;
+  const int cls = td.cls & 0xFF;
+  SplitK sk;
+  sk.ks0 = td.ks0;
+  sk.nst = td.ks1 - td.ks0;
+  sk.idx = (td.cls >> 8) & 0xFF;
+  sk.nsplit = (td.cls >> 16) & 0xFF;
+  sk.slab = td.slab;
+  sk.grp = td.grp;
+  sk.slabs = args.slabs;
+  sk.counters = args.counters;
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
-    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);  // no 64-row class
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);  // no 64-row class
   } else if constexpr ((ABL & 7) != 0) {
     return;  // ablation builds time the int8 path only
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
-    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);  // no 64-row class
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);  // no 64-row class
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
-    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v2<V2Cfg<64>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v2<V2Cfg<64>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
-    if (cls == 0) gg_tile_wo<WoCfg<256>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
-    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
-    else gg_tile_wo<WoCfg<64, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_wo<WoCfg<64, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
-    if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
-    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
-    else gg_tile_wo<WoCfg<64, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds);
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_wo<WoCfg<64, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   }
 }
 

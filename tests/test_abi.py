@@ -41,7 +41,7 @@ def test_struct_layouts():
 
 
 def test_abi_version_and_variants():
-    assert nat.lib().mxmoe_gg_abi_version() == 2
+    assert nat.lib().mxmoe_gg_abi_version() == 3
     vs = nat.list_variants()
     assert len(vs) == nat.variant_count() >= 1
     assert "w8a8_g-1_sym=TileConfig(" in vs[0]
@@ -132,3 +132,21 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     with pytest.raises(nat.NativeLibraryError):
         nat.lib()
     monkeypatch.setattr(nat, "_lib", None)
+
+
+def test_splitk_planning():
+    """A lone long-K problem (one CU's worth of tiles) is split along K on the v2 kernels: the
+    workspace grows by the partial slabs; a full bs=8192 layer call is never split."""
+    def ws(ps, v):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.workspace_size(arr, len(ps), v)
+
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    v2s, v3 = nat.default_variant(), names.index("v3_256x128_w4_dma_ring3_2wg")
+    lone = [_prob(M=512, N=2048, K=5632, a_bits=16, w_bits=16, scale_a=0, scale_b=0)]
+    assert ws(lone, v2s) > ws(lone, v3) + 16 * 256 * 1024  # >= 2 slices x 16 tiles x 256 KiB slabs
+    from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
+
+    layer = load_workload(qwen2_layer11_workload(8192))["layer-11"]["down"]
+    probs = [_prob(M=s.M, N=s.N, K=s.K, a_bits=16, w_bits=16, scale_a=0, scale_b=0) for s in layer]
+    assert ws(probs, v2s) < 1 << 20  # table only

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from mxmoe_amd import _native as nat
-from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, GroupGemm, group_gemm, groupgemm_reference_abi
+from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, GroupGemm, QParams, group_gemm, groupgemm_reference_abi
 from tests._util import HostProblem, assert_f16_close
 
 pytestmark = pytest.mark.gpu
@@ -23,7 +23,7 @@ DEV = "cuda"
 def _check(hps):
     for hp in hps:
         out, ref = hp.result(), hp.expected()
-        if hp.q.is_quant:
+        if hp.q.is_quant and not hp.q.is_weight_only:  # int32 accumulation: bit-exact
             mism = np.count_nonzero(out.view(np.uint16) != ref.view(np.uint16))
             assert mism == 0, f"{hp.q.qcfg} M={hp.M} N={hp.N} K={hp.K}: {mism} mismatching outputs"
         else:
@@ -164,3 +164,23 @@ def test_nslice_views_match_full_call():
         for i, (p, r) in enumerate(zip(full.problems, ref)):
             if p.M:
                 assert torch.equal(p.C.view(torch.int16), r.view(torch.int16)), (world, i)
+
+
+@pytest.mark.parametrize("q", [FP16, W8A8, W4A4, QParams(16, 4, 128, False)], ids=["fp16", "w8a8", "w4a4", "w4a16g128"])
+def test_splitk_long_k_low_fill(q):
+    """Low-fill calls with a long K (the shared expert's down at small batch) are split along K;
+    the last slice reduces the partial slabs in slice order: int paths stay bit-exact, results
+    are deterministic, and the arrival counters reset for the next launch."""
+    specs = [(512, 2048, 5632), (40, 2048, 1408), (3, 256, 1408)]
+    hps = [HostProblem(M, N, K, q, seed=90 + i, device=DEV) for i, (M, N, K) in enumerate(specs)]
+    gg = GroupGemm([h.problem for h in hps])
+    assert gg.info.splitk_slabs > 0
+    gg.launch()
+    torch.cuda.synchronize()
+    _check(hps)
+    first = [h.problem.C.clone() for h in hps]
+    for _ in range(3):
+        gg.launch()
+    torch.cuda.synchronize()
+    for h, c in zip(hps, first):
+        assert torch.equal(h.problem.C.view(torch.int16), c.view(torch.int16))
