@@ -153,6 +153,13 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
  * scale/zp pairs asym). */
 int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bits, uint8_t* out);
 
+/* Diagnostics (no reference counterpart): the tile timeline the "abl_v2s_trace" variant records,
+ * 4 uint64 per block {start, mainloop end, end after its stores drained (s_memrealtime, 100 MHz
+ * ticks), K stages << 48 | height class << 40 | qtype << 36 | XCC_ID << 32 | HW_ID} for the first
+ * 32768 blocks of the last traced launch. Copies
+ * min(bytes, 1 MiB) into host memory `dst` (synchronous); reset != 0 then zeroes the record. */
+int mxmoe_gg_debug_trace(void* dst, size_t bytes, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,7 +74,7 @@ EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
     "mxmoe_gg_variant_tile", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
-    "groupgemm_mxmoe", "mxmoe_gg_repack_weightonly",
+    "groupgemm_mxmoe", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
 )
 
 _lib = None
@@ -108,6 +108,8 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                          c.POINTER(MxmoeQParams), c.c_int]
     lib.mxmoe_gg_repack_weightonly.restype = c.c_int
     lib.mxmoe_gg_repack_weightonly.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
+    lib.mxmoe_gg_debug_trace.restype = c.c_int
+    lib.mxmoe_gg_debug_trace.argtypes = [c.c_void_p, c.c_size_t, c.c_int]
 
 
 def lib() -> ctypes.CDLL:

@@ -182,6 +182,7 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | ABL_NO_DMA>("abl_v2s_nodma"),
       make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
       make_v2<V2_STAGGER | ABL_NO_DMA | ABL_NO_EPI>("abl_v2s_nodma_noepi"),
+      make_v2<V2_STAGGER | V2_TRACE>("abl_v2s_trace"),
   };
   return v;
 }
@@ -711,6 +712,18 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
   return mxmoe_gg_launch(&info, nullptr);
 }
 
+
+int mxmoe_gg_debug_trace(void* dst, size_t bytes, int reset) {
+  const size_t n = std::min(bytes, sizeof(g_gg_trace));
+  if (dst && n) HIP_TRY(hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gg_trace), n, 0, hipMemcpyDeviceToHost));
+  if (reset) {
+    void* p = nullptr;
+    HIP_TRY(hipGetSymbolAddress(&p, HIP_SYMBOL(g_gg_trace)));
+    HIP_TRY(hipMemset(p, 0, sizeof(g_gg_trace)));
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  return MXMOE_GG_OK;
+}
 
 // Inverse of the reference's permute_weight(Row) + pack_weightonly (quantize.cuh:318-421), then
 // the kernel layout (include/mxmoe_gg.h). Host code, run once per weight at load time.

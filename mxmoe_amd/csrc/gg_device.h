@@ -460,8 +460,18 @@ __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& 
 
 // ABL flags. Timing ablations (results are garbage): 1 = no mainloop DMA (stage 0 reused),
 // 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores.
-// Option (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3.
-enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8 };
+// Options (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3;
+// 64 = tile timeline trace (diagnostics).
+enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8, V2_TRACE = 64 };
+
+// Tile timeline (diagnostics, V2_TRACE builds only): per block {start, mainloop end, end (stores
+// drained), nst << 48 | class << 40 | qtype << 36 | XCC_ID << 32 | HW_ID}, s_memrealtime ticks
+// (100 MHz); read back with mxmoe_gg_debug_trace.
+constexpr int kTraceBlocks = 32768;
+__device__ uint64_t g_gg_trace[kTraceBlocks * 4];
+__device__ __forceinline__ void trace_mark(int slot) {
+  if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) g_gg_trace[blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
+}
 
 // One 64-B K half of a v2 stage (128-B rows, XOR-swizzled 16-B chunks) as raw fragment words:
 // read from LDS, then consumed by the MFMAs (int4 widened at use). Used by the staggered v2
@@ -696,6 +706,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
   }
 
+  if constexpr ((ABL & V2_TRACE) != 0) trace_mark(1);
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
 
   // ---- epilogue: per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
@@ -1234,6 +1245,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
 __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
+  if constexpr ((ABL & V2_TRACE) != 0) trace_mark(0);
   const TileDesc td = args.tiles[blockIdx.x];
   if (td.prob < 0) return;
   const GGMeta mt = args.meta[td.prob];
@@ -1274,6 +1286,16 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
     if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_wo<WoCfg<64, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  }
+  if constexpr ((ABL & V2_TRACE) != 0) {
+    if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) {
+      wait_vmcnt<0>();
+      uint64_t hw = ((uint64_t)(__builtin_amdgcn_s_getreg((19 << 11) | 20) & 0xF) << 32) |  // XCC_ID
+                    ((uint64_t)(mt.qtype & 0xF) << 36) | ((uint64_t)(cls & 0xFF) << 40) |
+                    ((uint64_t)(sk.nst & 0xFFFF) << 48) | (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+      g_gg_trace[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+      g_gg_trace[blockIdx.x * 4 + 3] = hw;
+    }
   }
 }
 

@@ -1,7 +1,7 @@
 """Launch one GroupGEMM call repeatedly (for rocprofv3 counter runs / A-B of variants).
 
 python tools/kbench.py --cfg w8a8 --gg gate_up --variants 0,3 --iters 20 [--only shared|routed|all]
-(--variants auto = the library's AUTO choice)
+(--variants auto = the library's AUTO choice; 8@MXMOE_GG_XCD_BALANCE=0 = variant 8 planned with that env)
 """
 from __future__ import annotations
 
@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 from mxmoe_amd.groupgemm import GroupGemm  # noqa: E402
 from mxmoe_amd.harness import build_layer_inputs, time_launches  # noqa: E402
-from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload  # noqa: E402
+from mxmoe_amd.workload import QShape, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload  # noqa: E402
 
 
 def main():
@@ -32,19 +32,38 @@ def main():
     ap.add_argument("--rounds", type=int, default=5, help="round-robin rounds over the variants")
     ap.add_argument("--bs", type=int, default=8192, help="tokens (routed M_e scale with it)")
     ap.add_argument("--settle-s", type=float, default=1.0, help="seconds of load before timing")
+    ap.add_argument("--dense", default="", help="M,N,K: one dense problem (fp16 / w8a8 / w4a4) instead of the layer")
     args = ap.parse_args()
     kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
           "mixed": dict(qconfig=mixed_qconfig_lp1()), "w4a16": dict(qstr="w4a16_g128_asym"),
           "w4a16c": dict(qstr="w4a16_g-1_sym"), "w8a16": dict(qstr="w8a16_g-1_asym"),
           "w4a16ga": dict(qstr="w4a16_g-1_asym"), "w4a16gs": dict(qstr="w4a16_g128_sym")}[args.cfg]
-    shapes = load_workload(qwen2_layer11_workload(args.bs, **kw))["layer-11"][args.gg]
+    if args.dense:
+        bits = {"fp16": 16, "w8a8": 8, "w4a4": 4}[args.cfg]
+        shapes = [QShape([int(x) for x in args.dense.split(",")], bits, bits)]
+        args.gg = "dense_" + args.dense.replace(",", "x")
+    else:
+        shapes = load_workload(qwen2_layer11_workload(args.bs, **kw))["layer-11"][args.gg]
     if args.only == "shared":
         shapes = shapes[-1:]
     elif args.only == "routed":
         shapes = shapes[:-1]
     inp = build_layer_inputs(shapes)
-    ggs = [GroupGemm(inp.problems, variant=None if x == "auto" else int(x))  # None: MXMOE_GG_VARIANT_AUTO
-           for x in args.variants.split(",")]
+    ggs, labels = [], []
+    for spec in args.variants.split(","):  # "8", "auto", or "8@ENV=value" (planned with ENV set)
+        x, _, env = spec.partition("@")
+        saved = {}
+        if env:
+            k, val = env.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = val
+        ggs.append(GroupGemm(inp.problems, variant=None if x == "auto" else int(x)))  # None: AUTO
+        labels.append(spec)
+        for k, old in saved.items():
+            if old is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = old
     # A/B without order bias: ~1 s of sustained load first (clocks settle), then round-robin rounds
     # over the variants; per-variant median over every round's samples
     t0 = time.perf_counter()
@@ -58,9 +77,9 @@ def main():
         for k, gg in enumerate(ggs):
             t = time_launches(gg.launch, warmup=1, iters=per_round)
             samples[k].append(t["median_ms"])
-    for gg, ts in zip(ggs, samples):
+    for gg, ts, lab in zip(ggs, samples, labels):
         med = statistics.median(ts)
-        print(json.dumps({"variant": gg.variant, "cfg": args.cfg, "gg": args.gg, "only": args.only,
+        print(json.dumps({"variant": gg.variant, "spec": lab, "cfg": args.cfg, "gg": args.gg, "only": args.only,
                           "median_ms": round(med, 4), "spread_ms": round(max(ts) - min(ts), 4),
                           "tiles": gg.total_tiles, "grid": gg.info.grid,
                           "tflops": round(inp.flops / (med * 1e-3) / 1e12, 1),
