@@ -183,6 +183,7 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
       make_v2<V2_STAGGER | ABL_NO_DMA | ABL_NO_EPI>("abl_v2s_nodma_noepi"),
       make_v2<V2_STAGGER | V2_TRACE>("abl_v2s_trace"),
+      make_v2<V2_STAGGER | ABL_DMA_HOT>("abl_v2s_dmahot"),
   };
   return v;
 }

@@ -396,6 +396,39 @@ __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
 
+// Scaled int epilogue for the 4 columns of one accumulator fragment row:
+//   fp16_rn(0 + f32(acc >> SHIFT) * f32(fp16_rn(sa * sb[c])))   (the reference's arithmetic, gg_tile)
+// v_pk_mul_f16 forms two scale products at once (sa broadcast by op_sel_hi); v_fma_mix_f32 takes
+// the f16 product from either half of that register and computes f32(acc) * s + 0 with ONE
+// rounding, i.e. exactly the rounded f32 product, -0 turned into +0 as by the explicit add;
+// v_cvt_pk_f16_f32 rounds two results to fp16. 2.75 VALU per output instead of ~5.5.
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float mul_f32_f16lo(float a, uint32_t s) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(s));
+  return d;
+}
+__device__ __forceinline__ float mul_f32_f16hi(float a, uint32_t s) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(s));
+  return d;
+}
+template <int SHIFT>
+__device__ __forceinline__ uint2 scale_pack4(const v4i& acc, _Float16 sa, uint2 sbw) {
+  const h2_t sa2 = {sa, sa};
+  const uint32_t s01 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw.x));
+  const uint32_t s23 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw.y));
+  const h2_t lo = {(_Float16)mul_f32_f16lo((float)(acc[0] >> SHIFT), s01),
+                   (_Float16)mul_f32_f16hi((float)(acc[1] >> SHIFT), s01)};
+  const h2_t hi = {(_Float16)mul_f32_f16lo((float)(acc[2] >> SHIFT), s23),
+                   (_Float16)mul_f32_f16hi((float)(acc[3] >> SHIFT), s23)};
+  return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+}
+__device__ __forceinline__ uint2 pack4_f16(const v4f& acc) {
+  const h2_t lo = {(_Float16)acc[0], (_Float16)acc[1]}, hi = {(_Float16)acc[2], (_Float16)acc[3]};
+  return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -459,10 +492,11 @@ __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& 
 }
 
 // ABL flags. Timing ablations (results are garbage): 1 = no mainloop DMA (stage 0 reused),
-// 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores.
+// 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores, 16 = every stage's
+// LDS-DMA re-reads the tile's first K slice (same LDS traffic, L2-hot sources).
 // Options (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3;
 // 64 = tile timeline trace (diagnostics).
-enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8, V2_TRACE = 64 };
+enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8, ABL_DMA_HOT = 16, V2_TRACE = 64 };
 
 // Tile timeline (diagnostics, V2_TRACE builds only): per block {start, mainloop end, end (stores
 // drained), nst << 48 | class << 40 | qtype << 36 | XCC_ID << 32 | HW_ID}, s_memrealtime ticks
@@ -567,7 +601,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
     uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
     uint8_t* Bs = As + Cfg::A_BYTES;
-    const int kb = (ks0 + s) * Cfg::BKB;
+    const int kb = (ABL & ABL_DMA_HOT) ? ks0 * Cfg::BKB : (ks0 + s) * Cfg::BKB;
     if (kb + Cfg::BKB <= kbytes) {
 #pragma unroll
       for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
@@ -660,6 +694,20 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
   };
 
+  // int paths: row / column scales of the tile -> LDS (after the mainloop's LDS area). The load
+  // is issued with stage 0's DMA and written after the prologue barrier, so its latency hides
+  // under stage 0's and no register stays live across the mainloop.
+  _Float16 sc = 0;
+  if constexpr (QT != QT_F16) {
+    if (tid < Cfg::BM) sc = SA[min(m0 + tid, M - 1)];
+    else if (tid >= 256) sc = SB[min(n0 + tid - 256, N - 1)];
+  }
+  auto stash_scale = [&]() {
+    if constexpr (QT != QT_F16) {
+      if (tid < Cfg::BM || tid >= 256) reinterpret_cast<_Float16*>(lds + Cfg::LDS_BYTES)[tid] = sc;
+    }
+  };
+
   // ---- stagger (V2_STAGGER): SIMD partners are waves w and w+4 (a workgroup's waves go to the
   // SIMDs cyclically). In lockstep both read LDS, then both issue MFMAs, then meet at the barrier.
   // Waves 4-7 instead defer the second K half of every stage past the barrier, holding its
@@ -674,6 +722,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       Half fr;  // one fragment set (the late schedule carries it across the barrier)
       issue(0, 0);
       stage_sync(-1);
+      stash_scale();
       if (wave >= Cfg::WM * Cfg::WN / 2) {  // late: straight-line loop of its own
         for (int s = 0; s < nst; ++s) {
           if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
@@ -699,6 +748,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     // ---- mainloop: stage s+1 in flight (LDS-DMA) while stage s is consumed ----
     issue(0, 0);
     __syncthreads();  // vmcnt(0) + barrier: stage 0 landed for every wave
+    stash_scale();
     for (int s = 0; s < nst; ++s) {
       if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
       compute(s & 1);
@@ -706,48 +756,34 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
   }
 
+  if (nst <= 0) {  // no mainloop barrier behind the stash
+    stash_scale();
+    __syncthreads();
+  }
   if constexpr ((ABL & V2_TRACE) != 0) trace_mark(1);
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
 
   // ---- epilogue: per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
   uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
   const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
-  _Float16 sa[FM];
-  _Float16 sb[FN][4];
+  // int paths: the tile's row / column scales were staged in LDS during the prologue
+  const _Float16* sl = reinterpret_cast<const _Float16*>(lds + Cfg::LDS_BYTES);
+  uint2 sbw[FN];
   if constexpr (QT != QT_F16) {
-    // indices clamped (not predicated: a guarded load per element becomes a branch + wait each);
-    // values of rows / columns past M / N are never stored
 #pragma unroll
-    for (int i = 0; i < FM; ++i) sa[i] = SA[min(mrow0 + i * 16 + r16, M - 1)];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = min(ncol0 + j * 16 + 4 * g, N - 4);  // N % 8 == 0: a group of 4 is all in or all out
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sb[j][r] = SB[n + r];
-    }
+    for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * g);
   }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int ml = i * 16 + r16;
+    _Float16 sai = 0;
+    if constexpr (QT != QT_F16) sai = sl[wm * Cfg::WTM + ml];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      _Float16 h[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (QT == QT_F16) {
-          h[r] = (_Float16)acc[i][j][r];
-        } else {
-          constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
-          const _Float16 s16 = sa[i] * sb[j][r];
-          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
-          asm volatile("" : "+v"(prod));  // keep the f32 rounding of the product (see gg_tile)
-          h[r] = (_Float16)(0.0f + prod);
-        }
-      }
-      const int q = 2 * j + (g >> 1);
       uint2 pk;
-      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
-      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
+      if constexpr (QT == QT_F16) pk = pack4_f16(acc[i][j]);
+      else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
+      const int q = 2 * j + (g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
     }
   }
@@ -830,24 +866,10 @@ __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>:
     if constexpr (QT != QT_F16) sai = SA[min(mrow0 + ml, M - 1)];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      _Float16 h[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (QT == QT_F16) {
-          h[r] = (_Float16)acc[i][j][r];
-        } else {
-          constexpr int SHIFT = (QT == QT_I4) ? 8 : 0;
-          const uint32_t w = (r < 2) ? sbw[j].x : sbw[j].y;
-          const _Float16 s16 = sai * __builtin_bit_cast(_Float16, (uint16_t)(w >> (16 * (r & 1))));
-          float prod = (float)(acc[i][j][r] >> SHIFT) * (float)s16;
-          asm volatile("" : "+v"(prod));
-          h[r] = (_Float16)(0.0f + prod);
-        }
-      }
-      const int q = 2 * j + (g >> 1);
       uint2 pk;
-      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
-      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
+      if constexpr (QT == QT_F16) pk = pack4_f16(acc[i][j]);
+      else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
+      const int q = 2 * j + (g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * RB + ((q ^ (ml & (CPR - 1))) << 4) + (g & 1) * 8) = pk;
     }
   }
@@ -1244,7 +1266,8 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
 __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES];
+  // + the int paths' scale stash: SA at [LDS_BYTES, +2*BM), SB at [LDS_BYTES + 512, +512)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES + 1024];
   if constexpr ((ABL & V2_TRACE) != 0) trace_mark(0);
   const TileDesc td = args.tiles[blockIdx.x];
   if (td.prob < 0) return;
