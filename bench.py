@@ -40,6 +40,9 @@ CONFIGS = {
                   name="qwen2_moe layer-11 mixed w4a4+w8a8 (wbits=5.0, LP-1 qconfig) bs=8192"),
     "ds2_mixed": dict(kw="ds2_mixed", peak="int8", dtype="int4+int8",
                       name="DeepSeek-V2-Lite MoE layer mixed w4a4+w8a8 (25 % w8a8 units) bs=8192, 64 experts"),
+    # w4a4 g128: int4 A / B, one scale per 128-K group, f32 fold per group
+    "w4a4_g128": dict(kw=dict(qstr="w4a4_g128_sym"), peak="int8", dtype="int4 (g128)",
+                      name="qwen2_moe layer-11 w4a4_g128_sym GroupGEMM bs=8192 (int8 MFMA + per-group f32 fold)"),
     # weight-only: fp16 activations, int4 weights dequantised to fp16 MFMA
     "w4a16": dict(kw=dict(qstr="w4a16_g128_asym"), peak="fp16", dtype="fp16 (int4 weights)",
                   name="qwen2_moe layer-11 w4a16_g128_asym GroupGEMM bs=8192"),

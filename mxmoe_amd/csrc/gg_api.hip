@@ -77,7 +77,7 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   if constexpr ((ABL & 7) != 0) {
     launch_v2_q<ABL, 7>(a, grid, s);
   } else {
-    switch (qmask & 31) {
+    switch (qmask & 63) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
       case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
       case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
@@ -85,9 +85,10 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       case 7: launch_v2_q<ABL, 7>(a, grid, s); break;
       case 8: launch_v2_q<ABL, 8>(a, grid, s); break;    // w4a16 only
       case 16: launch_v2_q<ABL, 16>(a, grid, s); break;  // w8a16 only
+      case 32: launch_v2_q<ABL, 32>(a, grid, s); break;  // w4a4 g128 only
       // any other mix: every tile body in one kernel. The staggered int bodies leave no register
       // room for that (the compiler spilled inside their K loops), so the fallback is plain v2.
-      default: launch_v2_q<0, 31>(a, grid, s); break;
+      default: launch_v2_q<0, 63>(a, grid, s); break;
     }
   }
 }
@@ -116,7 +117,7 @@ Variant make_v0(const char* name) {
   v.geom[QT_F16] = {C16::BM, C16::BN, C16::BKB, C16::kThreads};
   v.geom[QT_I8] = {C8::BM, C8::BN, C8::BKB, C8::kThreads};
   v.geom[QT_I4] = {C4::BM, C4::BN, C4::BKB, C4::kThreads};
-  v.geom[QT_W4A16] = v.geom[QT_W8A16] = {0, 0, 0, 0};  // weight-only: v2 kernels only
+  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = C16::kThreads;
   v.lds_bytes = FusedCfg<C16, C8, C4>::LDS_BYTES;
   v.chunk = FusedCfg<C16, C8, C4>::LDS_BYTES <= 80 * 1024 ? 64 : 32;  // workgroups per XCD at once
@@ -133,7 +134,7 @@ Variant make_v3(const char* name) {
   v.name = name;
   v.kind = Kind::V3;
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};
-  v.geom[QT_W4A16] = v.geom[QT_W8A16] = {0, 0, 0, 0};  // weight-only: v2 kernels only
+  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = CT::NT;
   v.lds_bytes = CT::LDS_BYTES;
   v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
@@ -151,6 +152,7 @@ Variant make_v2(const char* name) {
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 128, 512};
   v.geom[QT_W4A16] = {256, 256, 32, 512};  // 64-K stages: 32 B of 4-bit codes per row
   v.geom[QT_W8A16] = {256, 256, 64, 512};
+  v.geom[QT_I4G] = {128, 256, 128, 512};  // w4a4 g128: 128-row tiles only (gg_tile_g128)
   v.threads = 512;
   v.lds_bytes = V2Cfg<256>::LDS_BYTES;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
@@ -212,6 +214,10 @@ int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
   }
   if (a_bits == 4 && w_bits == 4 && gsize == -1 && sym) {
     *qt = QT_I4;
+    return MXMOE_GG_OK;
+  }
+  if (a_bits == 4 && w_bits == 4 && gsize == 128 && sym) {  // w4a4_g128_sym (cta_gemm.cuh:610-772)
+    *qt = QT_I4G;
     return MXMOE_GG_OK;
   }
   if (a_bits == 16 && (w_bits == 4 || w_bits == 8)) {  // weight-only; group size checked per problem
@@ -304,6 +310,8 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (v.k_stage_bytes && (kbits / 8) % v.k_stage_bytes != 0)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: variant %s needs K*bits/8 to be a multiple of %d bytes (K=%d)",
                 idx, v.name, v.k_stage_bytes, p.K);
+  if (qt == QT_I4G && p.K % 128 != 0)
+    return fail(MXMOE_GG_ERR_INVALID, "problem %d: w4a4_g128 needs K %% 128 == 0 (K=%d)", idx, p.K);
   if (qt != QT_F16 && p.K > 131072)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d exceeds the exact int32 accumulation bound 131072", idx, p.K);
   if (p.N % 8 != 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: N=%d must be a multiple of 8", idx, p.N);
@@ -329,6 +337,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   m->qtype = qt;
   m->tiles_n = (p.N + v.geom[qt].bn - 1) / v.geom[qt].bn;
   m->kbytes = (int32_t)kbytes;
+  m->reserved = qt == QT_I4G ? p.K / 128 : 0;  // w4a4 g128: scale groups
   m->lda_b = lda_b;
   m->ldb_b = ldb_b;
   m->ldc = ldc;
@@ -369,7 +378,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   };
   auto full_tile_cost = [&](int i) {
     const GGMeta& m = all[i];
-    const double passes = m.qtype == QT_I4 ? 2.0 : 1.0;  // int4: 2 MFMA passes per staged byte
+    // int4: 2 MFMA passes per staged byte; g128 adds the per-group f32 fold (~25 %)
+    const double passes = m.qtype == QT_I4 ? 2.0 : m.qtype == QT_I4G ? 2.5 : 1.0;
     return passes * (double)m.kbytes * v.geom[m.qtype].bm * v.geom[m.qtype].bn;
   };
   // m-tiles of a problem: (m0, class); v2 classes 256 / 128 / 64 rows (see Variant::tail_bm)
@@ -380,7 +390,10 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
       const bool small_class = m.qtype == QT_F16 || m.qtype == QT_W4A16 || m.qtype == QT_W8A16;
-      if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
+      if (m.qtype == QT_I4G) {  // one 128-row tile body (class 1) for every m-tile
+        mt.push_back({m0, 1});
+        m0 += g.bm;
+      } else if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
         mt.push_back({m0, 2});
         m0 += v.tail2_bm;
       } else if (v.kind != Kind::V0 && v.tail_bm && rem <= v.tail_bm) {
@@ -413,7 +426,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     const double share = total / kSplitCUs;
     for (int i : order) {
       const double ratio = biggest[i] / std::max(share, 1.0);
-      if (ratio > 2.0) split[i] = std::max(1, std::min({8, (int)ratio, stages_of(all[i]) / 4}));
+      // (w4a4 g128 never splits: summing f32 partial folds would change the rounding)
+      if (ratio > 2.0 && all[i].qtype != QT_I4G) split[i] = std::max(1, std::min({8, (int)ratio, stages_of(all[i]) / 4}));
     }
   }
   auto tile_cost = [&](int i) { return full_tile_cost(i) / split[i]; };
@@ -541,8 +555,8 @@ int mxmoe_gg_default_variant(void) { return variant_index(kDefaultVariantName); 
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
   // weight-only kernels cover every group size / sym of a bit width: listed under the base name
-  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16", "w8a16"};
-  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8};
+  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16", "w8a16", "w4a4_g128_sym"};
+  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4};
   std::string out;
   const auto& vs = variants();
   for (size_t i = 0; i < vs.size(); ++i) {

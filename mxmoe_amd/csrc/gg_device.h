@@ -31,7 +31,8 @@
 
 namespace mxmoe {
 
-enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_COUNT = 5 };
+// QT_I4G: w4a4_g128_sym (A and B int4 with one fp16 scale per 128-K group)
+enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_I4G = 5, QT_COUNT = 6 };
 
 // One row of the plan table (64 B), written by the host planner into the workspace.
 struct GGMeta {
@@ -801,6 +802,211 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   }
 }
 
+// ============================================================================================
+// w4a4 g128 (reference cta_gemm_w4a4g128, cta_gemm.cuh:610-772, Atom-style): per 128-K group an
+// exact int32 dot product, folded into an f32 accumulator in group order,
+//     out = fma(f32(acc_g), f32(fp16_rn(sa_g[m] * sb_g[n])), out),   C = fp16_rn(out)
+// (`frag_out += T(acc) * T(sa * sb)`, mm_tile.cuh:490-493, which nvcc contracts to one FFMA).
+// Scales: fp16 [K/128][M] and [K/128][N] (permute_scale, quantize.cuh:299-315; test.cu:283-313).
+//
+// MI355X layout: the 128-row v2 tile (8 waves 2M x 4N, wave tile 64 x 64) — the int32 group
+// accumulators and the f32 fold accumulators both live in registers, which a 128 x 64 wave tile
+// would not fit. One 128-B K stage = 256 int4 = two groups: MFMA steps 0-1 form group 2s, steps
+// 2-3 group 2s+1, each group's first MFMA starting from a zero accumulator operand. The widened
+// nibbles make acc = 256 * sum(a*b) (exact, |acc| < 2^22); the fold runs on that raw value and the
+// store multiplies by 2^-8 — power-of-two scaling commutes with every rounding here (all partial
+// values are multiples of 2^-16, far from f32 under/overflow), so the result is the reference's
+// bit for bit, for 2.5 VALU per output per group (v_cvt_f32_i32, v_fma_mix_f32, half a
+// v_pk_mul_f16). Group scales of stage s+1 are loaded (one or two halves per thread) before that
+// stage's DMA, written to a 1.5-KiB LDS slot after stage s's MFMAs, and published by the stage
+// barrier. Not split along K (an f32 partial sum would change the rounding order).
+// ============================================================================================
+__device__ __forceinline__ float fma_f32_f16lo(float a, uint32_t s, float c) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(s), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float fma_f32_f16hi(float a, uint32_t s, float c) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(s), "v"(c));
+  return d;
+}
+
+template <class Cfg>
+__device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __restrict__ A,
+                                             const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
+                                             const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
+                                             uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
+  static_assert(Cfg::BM <= 256 && Cfg::BN == 256, "scale slot holds 256 rows / columns per group");
+  constexpr int SCL = 2 * Cfg::STAGE_BYTES;  // LDS scale slots: [buf][sa 2 x 256 | sb 2 x 256] fp16
+  constexpr int SCL_BYTES = 2048;
+  static_assert(SCL + 2 * SCL_BYTES <= V2Cfg<256>::LDS_BYTES, "scale slots must fit the v2 LDS image");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N, kbytes = mt.kbytes, ngroups = mt.reserved;
+  const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
+  const int nst = (kbytes + Cfg::BKB - 1) / Cfg::BKB;
+
+  const uint8_t* srcA[GA];
+  const uint8_t* srcB[GB];
+  {
+    const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int row = (wave * GA + j) * 8 + rsub;
+      srcA[j] = A + (int64_t)min(m0 + row, M - 1) * lda + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = (wave * GB + j) * 8 + rsub;
+      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+  }
+  auto issue = [&](int s, int buf) {
+    uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
+    uint8_t* Bs = As + Cfg::A_BYTES;
+    const int kb = s * Cfg::BKB;
+    if (kb + Cfg::BKB <= kbytes) {
+#pragma unroll
+      for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
+    } else {  // K tail: the second group of the last stage does not exist; its chunks load zeros
+      const int rsub = lane >> 3, p = lane & 7;
+      const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const int kc = (p ^ ((((wave * GA + j) * 8 + rsub) >> 1) & 7)) << 4;
+        glds16(kb + kc < kbytes ? srcA[j] + kb : zero, As + (wave * GA + j) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int kc = (p ^ ((((wave * GB + j) * 8 + rsub) >> 1) & 7)) << 4;
+        glds16(kb + kc < kbytes ? srcB[j] + kb : zero, Bs + (wave * GB + j) * 1024);
+      }
+    }
+  };
+  // group scales of stage s: threads 0-255 one sa value (group tid >> 7, row tid & 127 — BM <= 128
+  // rows used), threads 256-511 the two sb values of column tid - 256
+  uint32_t sc = 0;
+  auto load_scales = [&](int s) {
+    const int g0 = 2 * s;
+    if (tid < 256) {
+      const int gg = g0 + (tid >> 7), r = tid & 127;
+      if (gg < ngroups && r < Cfg::BM) sc = __builtin_bit_cast(uint16_t, SA[(int64_t)gg * M + min(m0 + r, M - 1)]);
+    } else {
+      const int n = min(n0 + tid - 256, N - 1);
+      const uint32_t lo = __builtin_bit_cast(uint16_t, SB[(int64_t)g0 * N + n]);
+      const uint32_t hi = g0 + 1 < ngroups ? __builtin_bit_cast(uint16_t, SB[(int64_t)(g0 + 1) * N + n]) : 0u;
+      sc = lo | (hi << 16);
+    }
+  };
+  auto stash_scales = [&](int buf) {
+    uint16_t* sl = reinterpret_cast<uint16_t*>(lds + SCL + buf * SCL_BYTES);
+    if (tid < 256) {
+      sl[(tid >> 7) * 256 + (tid & 127)] = (uint16_t)sc;
+    } else {
+      sl[512 + tid - 256] = (uint16_t)sc;
+      sl[768 + tid - 256] = (uint16_t)(sc >> 16);
+    }
+  };
+
+  v4f out[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) out[i][j] = v4f{0, 0, 0, 0};
+
+  const int swz = (r16 >> 1) & 7;
+  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
+  const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
+  auto compute = [&](int buf, int s) {
+    const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
+    const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
+    const _Float16* sl = reinterpret_cast<const _Float16*>(lds + SCL + buf * SCL_BYTES);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && 2 * s + 1 >= ngroups) break;  // K tail: no second group in this stage
+      v4i acc[FM][FN];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int st = 2 * h + t;
+        const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
+        v4i a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], t == 0 ? v4i{0, 0, 0, 0} : acc[i][j], 0, 0, 0);
+      }
+      // fold: out += f32(acc) * f32(fp16_rn(sa * sb)) with one rounding (v_fma_mix_f32)
+      const _Float16* sa = sl + h * 256 + wm * Cfg::WTM + r16;
+      const uint2* sbp = reinterpret_cast<const uint2*>(sl + 512 + h * 256 + wn * Cfg::WTN + 4 * g);
+      uint2 sbw[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) sbw[j] = sbp[j * 4];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const _Float16 sai = sa[i * 16];
+        const h2_t sa2 = {sai, sai};
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const uint32_t s01 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw[j].x));
+          const uint32_t s23 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw[j].y));
+          out[i][j][0] = fma_f32_f16lo((float)acc[i][j][0], s01, out[i][j][0]);
+          out[i][j][1] = fma_f32_f16hi((float)acc[i][j][1], s01, out[i][j][1]);
+          out[i][j][2] = fma_f32_f16lo((float)acc[i][j][2], s23, out[i][j][2]);
+          out[i][j][3] = fma_f32_f16hi((float)acc[i][j][3], s23, out[i][j][3]);
+        }
+      }
+    }
+  };
+
+  if (nst > 0) {
+    load_scales(0);
+    issue(0, 0);
+    stash_scales(0);  // waits for the scale loads only (issued before the DMA)
+    __syncthreads();  // stage 0 and its scales visible
+    for (int s = 0; s < nst; ++s) {
+      if (s + 1 < nst) {
+        load_scales(s + 1);  // before the DMA: the wait on them leaves the DMA in flight
+        issue(s + 1, (s + 1) & 1);
+      }
+      compute(s & 1, s);
+      if (s + 1 < nst) stash_scales((s + 1) & 1);  // slot last read by stage s-1 (before the last barrier)
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (as gg_tile_v2): out * 2^-8 (exact) -> fp16, per-wave LDS staging, 16-B stores ----
+  uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
+  const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = i * 16 + r16;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const uint2 pk = pack4_f16(out[i][j] * (1.0f / 256.0f));
+      const int q = 2 * j + (g >> 1);
+      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
+    }
+  }
+#pragma unroll 4
+  for (int it = 0; it < Cfg::WTM / 8; ++it) {
+    const int row = it * 8 + (lane >> 3), q = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
+    const int m = mrow0 + row, n = ncol0 + q * 8;
+    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+  }
+}
+
 // v2 fused kernel: qtype x height-class dispatch, uniform per workgroup.
 
 
@@ -1297,6 +1503,8 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);  // no 64-row class
+  } else if ((QM & (1 << QT_I4G)) && mt.qtype == QT_I4G) {
+    gg_tile_g128<V2Cfg<128>>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);  // 128-row tiles only
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);

@@ -59,13 +59,14 @@ class QParams:
 FP16 = QParams()
 W8A8 = QParams(8, 8, -1, True)
 W4A4 = QParams(4, 4, -1, True)
+W4A4_G128 = QParams(4, 4, 128, True)  # w4a4_g128_sym: one scale per 128-K group (cta_gemm.cuh:610-772)
 # weight-only (any group size that is -1 or a multiple of 64 dividing K, sym or asym, 4 / 8 bits)
 W4A16_G128_ASYM = QParams(16, 4, 128, False)
 W4A16_ASYM = QParams(16, 4, -1, False)
 W4A16_G128_SYM = QParams(16, 4, 128, True)
 W8A16_ASYM = QParams(16, 8, -1, False)
 
-SUPPORTED = {q.qcfg: q for q in (FP16, W8A8, W4A4, W4A16_G128_ASYM, W4A16_ASYM, W4A16_G128_SYM, W8A16_ASYM,
+SUPPORTED = {q.qcfg: q for q in (FP16, W8A8, W4A4, W4A4_G128, W4A16_G128_ASYM, W4A16_ASYM, W4A16_G128_SYM, W8A16_ASYM,
                                   QParams(16, 4, -1, True), QParams(16, 8, -1, True), QParams(16, 8, 128, True),
                                   QParams(16, 8, 128, False))}
 
@@ -75,7 +76,8 @@ class Problem:
     """One GroupGEMM problem  C[M,N] = A[M,K] . B[N,K]^T  on device tensors.
 
     fp16: A fp16 [M,K], B fp16 [N,K].  quant: A uint8 [M, K*a_bits/8] / B uint8 [N, K*w_bits/8]
-    in pack_wxax layout, scale_a fp16 [M], scale_b fp16 [N].  C fp16 [M, ldc] (ldc >= N).
+    in pack_wxax layout, scale_a fp16 [M], scale_b fp16 [N] (w4a4_g128: [K/128][M] and [K/128][N],
+    the permute_scale layout).  C fp16 [M, ldc] (ldc >= N).
     """
 
     A: torch.Tensor

@@ -44,7 +44,7 @@ class LayerInputs:
             if s.qcfg != "fp16" and ab == 16:  # weight-only: scale (+ zp) per column and group
                 tot += 2 * s.N * (1 if s.gsize == -1 else s.K // s.gsize) * (1 if s.sym else 2)
             elif s.qcfg != "fp16":
-                tot += 2 * (s.M + s.N)
+                tot += 2 * (s.M + s.N) * (1 if s.gsize == -1 else s.K // s.gsize)
         return tot
 
 
@@ -66,8 +66,8 @@ def build_layer_inputs(shapes: Sequence[QShape], device="cuda", seed: int = 42,
                                  scale_b=sz))
             del codes
         elif q.is_quant:
-            qa, sa = quant_rtn_sym(a, q.a_bits)
-            qb, sb = quant_rtn_sym(b, q.w_bits)
+            qa, sa = quant_rtn_sym(a, q.a_bits, q.gsize)
+            qb, sb = quant_rtn_sym(b, q.w_bits, q.gsize)
             A, B = pack_wxax(qa, q.a_bits), pack_wxax(qb, q.w_bits)
             del qa, qb
             probs.append(Problem(A=A, B=B, C=C, M=M, N=N, K=K, q=q, scale_a=sa, scale_b=sb))

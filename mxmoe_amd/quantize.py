@@ -27,18 +27,30 @@ def qmax_of(bits: int) -> int:
     return (1 << (bits - 1)) - 1
 
 
-def quant_rtn_sym(x: torch.Tensor, bits: int) -> tuple[torch.Tensor, torch.Tensor]:
-    """Per-row (gsize -1) symmetric RTN of an fp16 [rows, K] tensor -> (int8 codes, fp16 scale[rows])."""
+def quant_rtn_sym(x: torch.Tensor, bits: int, gsize: int = -1) -> tuple[torch.Tensor, torch.Tensor]:
+    """Symmetric RTN of an fp16 [rows, K] tensor -> (int8 codes [rows, K], fp16 scales).
+
+    gsize -1: one scale per row, scale [rows].  gsize g: one scale per (row, g-element K group), the
+    reference harness's quant_weight over [rows * K/g] blocks (test.cu:240-284) followed by
+    permute_scale (quantize.cuh:299-315): scale [K/g * rows], group-major ([K/g][rows])."""
     if x.dtype != torch.float16:
         raise TypeError("quant_rtn_sym expects fp16 input (the reference quantises in half)")
     if bits not in (4, 8):
         raise ValueError("only 4/8-bit WxAx quantisation is supported")
+    rows, K = x.shape
+    g = K if gsize == -1 else gsize
+    if g <= 0 or K % g:
+        raise ValueError(f"K={K} must be a multiple of the group size {gsize}")
     qmax = qmax_of(bits)
-    amax = x.abs().amax(dim=-1)
+    grp = x.reshape(rows, K // g, g)
+    amax = grp.abs().amax(dim=-1)
     scale = amax / qmax  # fp16 / int -> fp16, correctly rounded
     scale = torch.where(scale == 0, torch.ones_like(scale), scale)
-    q = (x / scale[..., None]).clamp(-qmax, qmax).round()  # round = half to even
-    return q.to(torch.int8), scale
+    q = (grp / scale[..., None]).clamp(-qmax, qmax).round()  # round = half to even
+    q = q.to(torch.int8).reshape(rows, K)
+    if gsize == -1:
+        return q, scale.reshape(rows)
+    return q, scale.t().contiguous().reshape(-1)
 
 
 def pack_wxax(q: torch.Tensor, bits: int) -> torch.Tensor:

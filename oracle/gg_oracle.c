@@ -10,6 +10,7 @@
  *   w8a8/w4a4     exact integer dot product over K ... cta_gemm.cuh:423-608 (int32 mma accumulate)
  *   epilogue      out = fp16_rn(0 + f32(acc) * f32(fp16_rn(sa[m]*sb[n])))
  *                 ............................... mm_tile.cuh:469-496 (scale_frag), 610-662 (store)
+ *   w4a4 g128     per-group int32 dot products folded with fmaf ... cta_gemm.cuh:610-772
  *   fp16          C = fp16_rn(sum_k a*b) with an f64 accumulator (the reference accumulates in
  *                 f32 on tensor cores, order unspecified: cta_gemm.cuh:7-107) — tolerance-checked.
  * The column-scale index uses the INTENDED sb[n] (SURVEY.md §8(a) a11 documents the reference's
@@ -181,6 +182,50 @@ int oracle_gg_quant(const uint8_t* A, const uint8_t* B, const uint16_t* sa, cons
       const uint16_t s16 = f16_mul(sa[m], sb[n]);
       const float v = 0.0f + (float)acc * oracle_f16_to_f32(s16);
       C[m * ldc + n] = oracle_f32_to_f16(v);
+    }
+    free(aq);
+  }
+  free(bq);
+  return rc;
+}
+
+/* ---- w4a4 g128 (group-quantised WxAx) problem: cta_gemm_w4a4g128, cta_gemm.cuh:610-772 ----
+ * Per group g of `gsize` K elements an exact int32 dot product acc_g, folded in group order into an
+ * f32 accumulator: out = fmaf(f32(acc_g), f32(fp16_rn(sa[g][m] * sb[g][n])), out), starting from
+ * +0 (frag_c_out{} then `frag_out += T(acc) * T(sa * sb)`, mm_tile.cuh:490-493 — nvcc's default
+ * --fmad contracts that into one FFMA); C = fp16_rn(out) (mm_tile.cuh:642-645).
+ * sa: [K/gsize][M], sb: [K/gsize][N] (permute_scale layout, quantize.cuh:299-315). */
+int oracle_gg_quant_grouped(const uint8_t* A, const uint8_t* B, const uint16_t* sa, const uint16_t* sb, uint16_t* C,
+                            int64_t M, int64_t N, int64_t K, int bits, int64_t gsize, int64_t lda_b, int64_t ldb_b,
+                            int64_t ldc, int nthreads) {
+  if (bits != 8 && bits != 4) return -1;
+  if (gsize <= 0 || K % gsize) return -2;
+  const int64_t G = K / gsize;
+  int8_t* bq = (int8_t*)malloc((size_t)(N * K > 0 ? N * K : 1));
+  if (!bq) return -3;
+  for (int64_t n = 0; n < N; ++n) unpack_row(B + n * ldb_b, bq + n * K, K, bits);
+  int rc = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t m = 0; m < M; ++m) {
+    int8_t* aq = (int8_t*)malloc((size_t)(K > 0 ? K : 1));
+    if (!aq) {
+      rc = -3;
+      continue;
+    }
+    unpack_row(A + m * lda_b, aq, K, bits);
+    for (int64_t n = 0; n < N; ++n) {
+      const int8_t* b = bq + n * K;
+      float out = 0.0f;
+      for (int64_t g = 0; g < G; ++g) {
+        int32_t acc = 0;
+        for (int64_t k = g * gsize; k < (g + 1) * gsize; ++k) acc += (int32_t)aq[k] * (int32_t)b[k];
+        const uint16_t s16 = f16_mul(sa[g * M + m], sb[g * N + n]);
+        out = fmaf((float)acc, oracle_f16_to_f32(s16), out);
+      }
+      C[m * ldc + n] = oracle_f32_to_f16(out);
     }
     free(aq);
   }

@@ -7,6 +7,7 @@ Every function restates reference arithmetic (SeaCatComplexes/MxMoE):
   quant_rtn_sym ....... quantize.cuh:218-279 (quant_weight), quant.py:40-84 (quant_minmax)
   pack / unpack ....... quantize.cuh:425-475 (pack_wxax)
   gg_quant ............ cta_gemm.cuh:423-608 + mm_tile.cuh:469-496, 610-662
+  gg_quant_grouped .... cta_gemm.cuh:610-772 (w4a4 g128: per-group int32 dot products, fmaf fold)
   gg_f16 .............. cta_gemm.cuh:7-107 (f64 accumulate here; tolerance-checked)
 """
 from __future__ import annotations
@@ -46,6 +47,8 @@ def lib() -> ctypes.CDLL:
         _lib.oracle_quant_rtn_sym.argtypes = [P, P, P, c.c_int64, c.c_int64, c.c_int]
         _lib.oracle_gg_quant.argtypes = [P, P, P, P, P, c.c_int64, c.c_int64, c.c_int64, c.c_int, c.c_int64,
                                          c.c_int64, c.c_int64, c.c_int]
+        _lib.oracle_gg_quant_grouped.argtypes = [P, P, P, P, P, c.c_int64, c.c_int64, c.c_int64, c.c_int, c.c_int64,
+                                                 c.c_int64, c.c_int64, c.c_int64, c.c_int]
         _lib.oracle_gg_f16.argtypes = [P, P, P, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64,
                                        c.c_int]
         _lib.oracle_max_threads.restype = c.c_int
@@ -75,6 +78,15 @@ def quant_rtn_sym(x_f16: np.ndarray, bits: int) -> tuple[np.ndarray, np.ndarray]
     return q, s
 
 
+def quant_rtn_sym_grouped(x_f16: np.ndarray, bits: int, gsize: int) -> tuple[np.ndarray, np.ndarray]:
+    """quant_weight over [rows * K/gsize] blocks of gsize K elements (test.cu:240-284), then
+    permute_scale (quantize.cuh:299-315): codes [rows, K], scales [K/gsize * rows] group-major."""
+    x = np.ascontiguousarray(x_f16, dtype=np.float16)
+    rows, K = x.shape
+    q, s = quant_rtn_sym(x.reshape(rows * (K // gsize), gsize), bits)
+    return q.reshape(rows, K), np.ascontiguousarray(s.reshape(rows, K // gsize).T).reshape(-1)
+
+
 def pack_wxax(q: np.ndarray, bits: int) -> np.ndarray:
     q = np.ascontiguousarray(q, dtype=np.int8)
     rows, K = q.shape
@@ -100,6 +112,20 @@ def gg_quant(A: np.ndarray, B: np.ndarray, sa: np.ndarray, sb: np.ndarray, M: in
     C = np.zeros((M, N), np.float16)
     kb = K * bits // 8
     _chk(lib().oracle_gg_quant(_p(A), _p(B), _p(sa), _p(sb), _p(C), M, N, K, bits, kb, kb, N, threads), "gg_quant")
+    return C
+
+
+def gg_quant_grouped(A: np.ndarray, B: np.ndarray, sa: np.ndarray, sb: np.ndarray, M: int, N: int, K: int,
+                     bits: int, gsize: int, threads: int = 0) -> np.ndarray:
+    """Expected fp16 C [M,N] of one group-quantised (w4a4 g128) problem; sa [K/g][M], sb [K/g][N]."""
+    A = np.ascontiguousarray(A, np.uint8)
+    B = np.ascontiguousarray(B, np.uint8)
+    sa = np.ascontiguousarray(sa, np.float16)
+    sb = np.ascontiguousarray(sb, np.float16)
+    C = np.zeros((M, N), np.float16)
+    kb = K * bits // 8
+    _chk(lib().oracle_gg_quant_grouped(_p(A), _p(B), _p(sa), _p(sb), _p(C), M, N, K, bits, gsize, kb, kb, N, threads),
+         "gg_quant_grouped")
     return C
 
 

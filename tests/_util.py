@@ -5,11 +5,11 @@ import numpy as np
 import torch
 
 from mxmoe_amd import _native as nat
-from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, Problem, QParams
+from mxmoe_amd.groupgemm import FP16, W4A4, W4A4_G128, W8A8, Problem, QParams
 from mxmoe_amd.quantize import pack_wxax, quant_rtn_sym
 from oracle import oracle, weightonly
 
-QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4}
+QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4, "w4a4_g128_sym": W4A4_G128}
 
 
 class HostProblem:
@@ -35,8 +35,8 @@ class HostProblem:
             self.sa = None
         elif q.is_quant:
             bits = q.a_bits
-            qa, sa = quant_rtn_sym(a, bits)
-            qb, sb = quant_rtn_sym(b, bits)
+            qa, sa = quant_rtn_sym(a, bits, q.gsize)
+            qb, sb = quant_rtn_sym(b, bits, q.gsize)
             self.qa, self.qb = qa.numpy(), qb.numpy()
             self.A = pack_wxax(qa, bits).numpy()
             self.B = pack_wxax(qb, bits).numpy()
@@ -63,6 +63,9 @@ class HostProblem:
         if self.q.is_weight_only:
             q = self.q
             return weightonly.gemm(self.A, weightonly.dequant(self.qb, self.sb, self.N, self.K, q.w_bits, q.gsize, q.sym))
+        if self.q.is_quant and self.q.gsize != -1:
+            return oracle.gg_quant_grouped(self.A, self.B, self.sa, self.sb, self.M, self.N, self.K, self.q.a_bits,
+                                           self.q.gsize)
         if self.q.is_quant:
             return oracle.gg_quant(self.A, self.B, self.sa, self.sb, self.M, self.N, self.K, self.q.a_bits)
         return oracle.gg_f16(self.A, self.B, self.M, self.N, self.K)

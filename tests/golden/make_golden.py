@@ -12,13 +12,16 @@ writes into the source tree, compose_kernel.py:556), with two shims that change 
                            (compose_kernel.py:87-132, tile_config.py:266-286)
   workload_golden.json ... generate_workload_from_gate_trace outputs (gen_workload.py:38-110)
   tile_repr_golden.json .. the exporter's repr of TileConfig tuples (bits_solver.py:30,67-68)
+  quant_g128_golden.npz .. quant_minmax(t, 4, 128, True) (group quantisation, quant.py:40-84)
+  gg_w4a4g128_small.npz .. w4a4_g128_sym vectors (inputs by quant_minmax gsize 128, expected C by an
+                           independent numpy restatement of the per-group fold, cta_gemm.cuh:610-772)
   gg_<kind>_small.npz .... GroupGEMM vectors: inputs quantised by the reference's quant_minmax,
                            packed per pack_wxax (quantize.cuh:425-475), expected C from an
                            independent numpy restatement (int64 matmul + epilogue mm_tile.cuh:469-496),
                            plus the reference-as-written column-scale permutation (mm_tile.cuh:452,462)
 The LP-derived mixed qconfig is solved exactly (0/1 knapsack DP) from bits_model-1.lp.
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [--only-g128]
 """
 from __future__ import annotations
 
@@ -188,9 +191,74 @@ def make_gg_vectors(ref, kind: str, specs, seed: int) -> dict:
     return out
 
 
+def fold_g128_np(qa: np.ndarray, qb: np.ndarray, sa: np.ndarray, sb: np.ndarray, gsize: int) -> np.ndarray:
+    """Independent numpy restatement of the w4a4 g128 epilogue (cta_gemm.cuh:610-772, mm_tile.cuh:490-493):
+    out = fma(f32(acc_g), f32(fp16(sa_g * sb_g)), out) per group in order, C = fp16(out). The fma is
+    formed in f64 (the product is exact there) and the f64 sum is checked exact by TwoSum, so the one
+    f32 rounding below is the fma's single rounding."""
+    M, K = qa.shape
+    N = qb.shape[0]
+    G = K // gsize
+    out = np.zeros((M, N), np.float32)
+    for g in range(G):
+        ks = slice(g * gsize, (g + 1) * gsize)
+        acc = qa[:, ks].astype(np.int64) @ qb[:, ks].astype(np.int64).T
+        s16 = (sa[g * M:(g + 1) * M].astype(np.float32)[:, None] *
+               sb[g * N:(g + 1) * N].astype(np.float32)[None, :]).astype(np.float16)
+        p = acc.astype(np.float64) * s16.astype(np.float64)
+        o = out.astype(np.float64)
+        t = p + o
+        bp = t - o
+        err = (p - bp) + (o - (t - bp))
+        assert (err == 0).all(), "f64 sum not exact: the restatement would double-round"
+        out = t.astype(np.float32)
+    return out.astype(np.float16)
+
+
+def make_g128_vectors(ref, specs, seed: int) -> dict:
+    """w4a4_g128_sym vectors: inputs quantised by the reference's quant_minmax(t, 4, 128, True)
+    (scales [rows*K/128] in (row, group) order, then permute_scale -> [K/128][rows])."""
+    g = torch.Generator().manual_seed(seed)
+    out = {"P": np.int32(len(specs))}
+    for i, (M, N, K) in enumerate(specs):
+        a = (torch.rand(M, K, generator=g) * 2 - 1).half()
+        b = (torch.rand(N, K, generator=g) * 2 - 1).half()
+        qa, sa, _ = ref.quant_minmax(a, 4, 128, True)
+        qb, sb, _ = ref.quant_minmax(b, 4, 128, True)
+        qa, qb = qa.to(torch.int8).numpy(), qb.to(torch.int8).numpy()
+        sa = np.ascontiguousarray(sa.reshape(M, K // 128).numpy().astype(np.float16).T).reshape(-1)
+        sb = np.ascontiguousarray(sb.reshape(N, K // 128).numpy().astype(np.float16).T).reshape(-1)
+        out[f"p{i}_shape"] = np.array([M, N, K], np.int32)
+        out[f"p{i}_bits"] = np.int32(4)
+        out[f"p{i}_qa"], out[f"p{i}_qb"] = qa, qb
+        out[f"p{i}_A"], out[f"p{i}_B"] = pack_np(qa, 4), pack_np(qb, 4)
+        out[f"p{i}_sa"], out[f"p{i}_sb"] = sa, sb
+        out[f"p{i}_C"] = fold_g128_np(qa, qb, sa, sb, 128)
+    return out
+
+
+def make_g128(ref):
+    """quant_g128_golden.npz (quant_minmax gsize 128 on seeded rows) + gg_w4a4g128_small.npz."""
+    qg = {}
+    g = torch.Generator().manual_seed(4321)
+    t = (torch.randn(17, 512, generator=g) * torch.logspace(-3, 1, 17)[:, None]).half()
+    t[2, 128:256] = 0.001 * t[2, 128:256]  # one tiny group
+    t[4, 300] = 9.0  # outlier inside one group
+    q, s, _ = ref.quant_minmax(t, 4, 128, True)
+    qg["x_4"] = t.numpy()
+    qg["q_4"] = q.to(torch.int8).numpy()
+    qg["scale_4"] = s.reshape(-1).numpy().astype(np.float16)  # (row, group) order, as quant_minmax returns
+    np.savez_compressed(HERE / "quant_g128_golden.npz", **qg)
+    specs = [(0, 256, 256), (1, 256, 128), (17, 128, 384), (130, 256, 1408), (257, 384, 256)]
+    np.savez_compressed(HERE / "gg_w4a4g128_small.npz", **make_g128_vectors(ref, specs, seed=128))
+
+
 def main():
     sys.path.insert(0, str(ROOT))
     ref = import_reference()
+    if "--only-g128" in sys.argv:
+        make_g128(ref)
+        return
     torch.manual_seed(0)
 
     # 1. quant_minmax golden
@@ -281,6 +349,7 @@ def main():
     mixed = [(130, 256, 256, "w8a8_g-1_sym"), (0, 128, 128, "w4a4_g-1_sym"), (77, 128, 512, "w4a4_g-1_sym"),
              (33, 256, 128, "fp16"), (257, 128, 256, "w8a8_g-1_sym"), (9, 256, 1024, "w4a4_g-1_sym")]
     np.savez_compressed(HERE / "gg_mixed_small.npz", **make_gg_vectors(ref, "mixed", mixed, 45))
+    make_g128(ref)
     print("golden fixtures written;", meta)
 
 
