@@ -75,7 +75,16 @@ EXPORTED_SYMBOLS = (
     "mxmoe_gg_list_variants",
     "mxmoe_gg_variant_tile", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
     "groupgemm_mxmoe", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
+    # include/mxmoe_moe.h (MoE-layer plumbing)
+    "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_combine",
 )
+
+
+class MoeSegC(ctypes.Structure):
+    """mxmoe_moe_seg (include/mxmoe_moe.h): one expert's segment of a permuted activation buffer."""
+
+    _fields_ = [("qtag", ctypes.c_int32), ("first_slot", ctypes.c_int32), ("rows", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("out_off", ctypes.c_int64), ("scale_off", ctypes.c_int64)]
 
 _lib = None
 
@@ -110,6 +119,15 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_repack_weightonly.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
     lib.mxmoe_gg_debug_trace.restype = c.c_int
     lib.mxmoe_gg_debug_trace.argtypes = [c.c_void_p, c.c_size_t, c.c_int]
+    P = c.c_void_p
+    lib.mxmoe_moe_route.restype = c.c_int
+    lib.mxmoe_moe_route.argtypes = [P, c.c_int64, c.c_int, c.c_int, P, P, P, P, P]
+    lib.mxmoe_moe_quant_act.restype = c.c_int
+    lib.mxmoe_moe_quant_act.argtypes = [P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, P, c.c_int, P, P, P]
+    lib.mxmoe_moe_silu_mul_quant.restype = c.c_int
+    lib.mxmoe_moe_silu_mul_quant.argtypes = [P, P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, c.c_int, P, P, P]
+    lib.mxmoe_moe_combine.restype = c.c_int
+    lib.mxmoe_moe_combine.argtypes = [P, P, P, P, P, c.c_int64, c.c_int, c.c_int, P, P]
 
 
 def lib() -> ctypes.CDLL:

@@ -543,6 +543,16 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
 
 }  // namespace
 
+namespace mxmoe {
+namespace detail {
+// error channel shared with the MoE plumbing (moe_ops.hip)
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+}  // namespace detail
+}  // namespace mxmoe
+
 extern "C" {
 
 int mxmoe_gg_abi_version(void) { return MXMOE_GG_ABI_VERSION; }

@@ -1,0 +1,364 @@
+// moe_ops.hip — MoE-layer plumbing around the GroupGEMM (include/mxmoe_moe.h), gfx950.
+//
+// Reference (SeaCatComplexes/MxMoE, mxmoe/kernels/src/ref_bind.cu; read as text only):
+//   gg_permute_inp: sort(topk_ids) / floor_divide(topk) / bincount ......... ref_bind.cu:47-64, 452-456
+//   quant_inp_act -> quant_act_kernel (per-expert activation quantisation) .. :434-592
+//   silu_mul_then_quant -> silu_mul_then_quant_kernel ....................... :595-757
+//   gg_unpermute_out (empty stub) ........................................... :66
+// The reference's device kernels (act_kernel.cuh) are absent from its tree; the quantiser here is
+// its quant_weight (quantize.cuh:218-279) per token row / 128-element group + pack_wxax
+// (quantize.cuh:425-475), i.e. exactly the operand format of the GroupGEMM.
+//
+// All four kernels are HBM-bound byte movers: one workgroup per row (token or slot), 16-B
+// coalesced loads of 8 fp16 per lane, reductions in registers / lane shuffles, stores of the packed
+// codes as one 4-B (int4) / 8-B (int8) / 16-B (fp16) word per lane — no LDS tiling, no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/mxmoe_gg.h"
+#include "../../include/mxmoe_moe.h"
+
+namespace mxmoe {
+namespace detail {
+int set_error(int code, const std::string& msg);  // gg_api.hip (thread-local mxmoe_gg_last_error)
+}
+
+namespace {
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return detail::set_error(code, buf);
+}
+
+constexpr int kThreads = 256;
+constexpr int kChunk = kThreads * 8;     // fp16 elements one pass of the workgroup covers
+constexpr int kMaxChunks = 8;            // rows up to 16384 elements
+constexpr int kMaxWidth = kChunk * kMaxChunks;
+
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// exclusive block prefix of v (256 threads) and the block total
+__device__ __forceinline__ int block_excl_scan(int v, int* total, int* lds4) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int incl = wave_incl_scan(v);
+  if (lane == 63) lds4[wave] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    base += w < wave ? lds4[w] : 0;
+    tot += lds4[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+__device__ __forceinline__ float block_max(float v, float* lds4) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  float m = lds4[0];
+#pragma unroll
+  for (int w = 1; w < kThreads / 64; ++w) m = fmaxf(m, lds4[w]);
+  return m;
+}
+
+// ---------------------------------------------------------------------------------------------
+// route: workgroup e finds every id == e in flattened order (stable), its slot base = #ids < e.
+// Each thread scans a contiguous run of the ids twice (count, then place); the runs' counts are
+// prefix-summed across the workgroup so the placement keeps the flattened order.
+__global__ __launch_bounds__(kThreads) void route_kernel(const int32_t* __restrict__ ids, int n, int topk,
+                                                         int32_t* __restrict__ sorted, int32_t* __restrict__ perm,
+                                                         int32_t* __restrict__ inv, int32_t* __restrict__ counts) {
+  __shared__ int lds4[kThreads / 64];
+  const int e = blockIdx.x;
+  const int per = (n + kThreads - 1) / kThreads;
+  const int b = threadIdx.x * per, end = min(n, b + per);
+  int less = 0, eq = 0;
+  for (int i = b; i < end; ++i) {
+    const int v = ids[i];
+    less += (v >= 0 && v < e);
+    eq += v == e;
+  }
+  int eq_total, less_total;
+  const int rank = block_excl_scan(eq, &eq_total, lds4);
+  block_excl_scan(less, &less_total, lds4);
+  if (threadIdx.x == 0) counts[e] = eq_total;
+  int pos = less_total + rank;
+  for (int i = b; i < end && eq > 0; ++i) {
+    if (ids[i] == e) {
+      sorted[pos] = e;
+      perm[pos] = i / topk;
+      inv[i] = pos;
+      ++pos;
+      --eq;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+struct ActArgs {
+  const _Float16* src;         // quant: hidden [T][K]; silu: routed gate_up [T*topk][2N]
+  const _Float16* src_shared;  // silu: shared gate_up [T][2Ns] (quant: = src)
+  int64_t ntk;                 // T * topk routed slots
+  int K;                       // quant: row width of hidden
+  int N, Ns;                   // silu: routed / shared intermediate width
+  const int32_t* sorted;
+  const int32_t* perm;
+  const mxmoe_moe_seg* segs;
+  int nseg;
+  uint8_t* out;
+  _Float16* scales;
+};
+
+__device__ __forceinline__ uint32_t pack_i8x4(int q0, int q1, int q2, int q3) {
+  // pack_wxax int8: word j = (q[2j] << 8) | q[2j+1] little-endian -> bytes q[2j+1], q[2j]
+  return (uint32_t)(q1 & 0xFF) | ((uint32_t)(q0 & 0xFF) << 8) | ((uint32_t)(q3 & 0xFF) << 16) |
+         ((uint32_t)(q2 & 0xFF) << 24);
+}
+__device__ __forceinline__ uint32_t pack_i4x8(const int (&q)[8]) {
+  // pack_wxax int4: word j = q[4j]<<12 | q[4j+1]<<8 | q[4j+2]<<4 | q[4j+3]
+  //   -> byte 2j = (q[4j+2] << 4) | q[4j+3], byte 2j+1 = (q[4j] << 4) | q[4j+1]
+  const uint32_t b0 = ((q[2] & 0xF) << 4) | (q[3] & 0xF), b1 = ((q[0] & 0xF) << 4) | (q[1] & 0xF);
+  const uint32_t b2 = ((q[6] & 0xF) << 4) | (q[7] & 0xF), b3 = ((q[4] & 0xF) << 4) | (q[5] & 0xF);
+  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+// quant_weight arithmetic (quantize.cuh:218-279): scale = fp16(amax / qmax), 0 -> 1;
+// q = rint_even(clamp(fp16(x / scale), -qmax, qmax))
+__device__ __forceinline__ _Float16 rtn_scale(float amax, float qmax) {
+  _Float16 s = (_Float16)(amax / qmax);
+  return s == (_Float16)0 ? (_Float16)1 : s;
+}
+__device__ __forceinline__ int rtn_code(_Float16 x, _Float16 s, float qmax) {
+  float d = (float)(_Float16)((float)x / (float)s);
+  d = fminf(fmaxf(d, -qmax), qmax);
+  return (int)__builtin_rintf(d);
+}
+
+template <bool SILU>
+__global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
+  __shared__ float lds4[kThreads / 64];
+  const int64_t s = blockIdx.x;
+  const int tid = threadIdx.x;
+  int e;
+  const _Float16* row_src;
+  if (s < a.ntk) {
+    e = a.sorted[s];
+    row_src = SILU ? a.src + s * 2 * (int64_t)a.N : a.src + (int64_t)a.perm[s] * a.K;
+  } else {
+    e = a.nseg - 1;
+    const int64_t t = s - a.ntk;
+    row_src = SILU ? a.src_shared + t * 2 * (int64_t)a.Ns : a.src + t * a.K;
+  }
+  if (e < 0 || e >= a.nseg) return;  // invalid id: the slot was never routed (route ignores it)
+  const mxmoe_moe_seg sg = a.segs[e];
+  const int64_t row = s - sg.first_slot;
+  if (row < 0 || row >= sg.rows) return;  // slot outside its segment (inconsistent table): never write
+  const int width = sg.width;
+  const int upoff = SILU ? (s < a.ntk ? a.N : a.Ns) : 0;  // column of the "up" half
+
+  h8_t x[kMaxChunks];
+#pragma unroll
+  for (int c = 0; c < kMaxChunks; ++c) {
+    const int idx = c * kChunk + tid * 8;
+    if (idx < width) {
+      if constexpr (SILU) {
+        const h8_t gv = *reinterpret_cast<const h8_t*>(row_src + idx);
+        const h8_t uv = *reinterpret_cast<const h8_t*>(row_src + upoff + idx);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float g = (float)gv[j];
+          x[c][j] = (_Float16)((g / (1.0f + expf(-g))) * (float)uv[j]);
+        }
+      } else {
+        x[c] = *reinterpret_cast<const h8_t*>(row_src + idx);
+      }
+    } else {
+      x[c] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  if (sg.qtag == MXMOE_ACT_FP16) {
+    _Float16* o = reinterpret_cast<_Float16*>(a.out + sg.out_off) + row * width;
+#pragma unroll
+    for (int c = 0; c < kMaxChunks; ++c) {
+      const int idx = c * kChunk + tid * 8;
+      if (idx < width) *reinterpret_cast<h8_t*>(o + idx) = x[c];
+    }
+    return;
+  }
+  const int bits = sg.qtag == MXMOE_ACT_INT8 ? 8 : 4;
+  const float qmax = bits == 8 ? 127.0f : 7.0f;
+  uint8_t* o = a.out + sg.out_off + row * (int64_t)width * bits / 8;
+  if (sg.qtag == MXMOE_ACT_INT4_G128) {
+    // 16 consecutive lanes hold one 128-element group of a chunk
+#pragma unroll
+    for (int c = 0; c < kMaxChunks; ++c) {
+      const int idx = c * kChunk + tid * 8;
+      if (c * kChunk >= width) break;  // uniform
+      float m = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)x[c][j]));
+#pragma unroll
+      for (int d = 8; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+      if (idx < width) {
+        const _Float16 sc = rtn_scale(m, qmax);
+        int q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, qmax);
+        *reinterpret_cast<uint32_t*>(o + idx / 2) = pack_i4x8(q);
+        if ((tid & 15) == 0) a.scales[sg.scale_off + (int64_t)(idx / 128) * sg.rows + row] = sc;
+      }
+    }
+    return;
+  }
+  float m = 0.0f;
+#pragma unroll
+  for (int c = 0; c < kMaxChunks; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)x[c][j]));
+  m = block_max(m, lds4);
+  const _Float16 sc = rtn_scale(m, qmax);
+  if (tid == 0) a.scales[sg.scale_off + row] = sc;
+#pragma unroll
+  for (int c = 0; c < kMaxChunks; ++c) {
+    const int idx = c * kChunk + tid * 8;
+    if (idx >= width) continue;
+    int q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, qmax);
+    if (bits == 8) {
+      *reinterpret_cast<uint2*>(o + idx) = uint2{pack_i8x4(q[0], q[1], q[2], q[3]), pack_i8x4(q[4], q[5], q[6], q[7])};
+    } else {
+      *reinterpret_cast<uint32_t*>(o + idx / 2) = pack_i4x8(q);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// combine: one workgroup per token, 8 fp16 columns per lane and pass
+__global__ __launch_bounds__(kThreads) void combine_kernel(const _Float16* __restrict__ y, const int32_t* __restrict__ inv,
+                                                           const float* __restrict__ w, const _Float16* __restrict__ shared,
+                                                           const float* __restrict__ shared_w, int topk, int H,
+                                                           _Float16* __restrict__ out) {
+  const int64_t t = blockIdx.x;
+  for (int idx = threadIdx.x * 8; idx < H; idx += kChunk) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < topk; ++k) {
+      const int64_t slot = inv[t * topk + k];
+      const float wk = w[t * topk + k];
+      const h8_t v = *reinterpret_cast<const h8_t*>(y + slot * H + idx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(wk, (float)v[j], acc[j]);
+    }
+    if (shared) {
+      const float ws = shared_w ? shared_w[t] : 1.0f;
+      const h8_t v = *reinterpret_cast<const h8_t*>(shared + t * H + idx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaf(ws, (float)v[j], acc[j]);
+    }
+    h8_t r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (_Float16)acc[j];
+    *reinterpret_cast<h8_t*>(out + t * H + idx) = r;
+  }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+}  // namespace mxmoe
+
+using namespace mxmoe;
+
+extern "C" {
+
+int mxmoe_moe_route(const int32_t* topk_ids, int64_t T, int topk, int E, int32_t* sorted_expert,
+                    int32_t* perm_token, int32_t* inv_slot, int32_t* counts, void* stream) {
+  if (T < 0 || topk <= 0 || E <= 0 || E > 4096 || T * topk > (int64_t)1 << 30)
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_route: bad sizes (T=%lld topk=%d E=%d)", (long long)T, topk, E);
+  if (T > 0 && (!topk_ids || !sorted_expert || !perm_token || !inv_slot))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_route: NULL pointer");
+  if (!counts) return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_route: NULL counts");
+  hipLaunchKernelGGL(route_kernel, dim3(E), dim3(kThreads), 0, (hipStream_t)stream, topk_ids, (int)(T * topk), topk,
+                     sorted_expert, perm_token, inv_slot, counts);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "route_kernel launch failed: %s", hipGetErrorString(e));
+  return MXMOE_GG_OK;
+}
+
+static int launch_act(bool silu, const ActArgs& a, int64_t nslots, void* stream) {
+  if (nslots == 0) return MXMOE_GG_OK;
+  if (silu) hipLaunchKernelGGL(act_quant_kernel<true>, dim3((unsigned)nslots), dim3(kThreads), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(act_quant_kernel<false>, dim3((unsigned)nslots), dim3(kThreads), 0, (hipStream_t)stream, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "act_quant_kernel launch failed: %s", hipGetErrorString(e));
+  return MXMOE_GG_OK;
+}
+
+int mxmoe_moe_quant_act(const void* hidden, int64_t T, int K, int topk, int with_shared,
+                        const int32_t* sorted_expert, const int32_t* perm_token, const mxmoe_moe_seg* segs, int nseg,
+                        void* out, void* scales, void* stream) {
+  if (T < 0 || topk <= 0 || nseg <= 0 || K <= 0 || K % 128 || K > kMaxWidth)
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_quant_act: need K %% 128 == 0, K <= %d, topk > 0, nseg > 0 (K=%d)",
+                kMaxWidth, K);
+  if (T > 0 && (!hidden || !sorted_expert || !perm_token || !segs || !out || !aligned16(hidden) || !aligned16(out)))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_quant_act: NULL or misaligned pointer (hidden / out need 16 B)");
+  const ActArgs a{static_cast<const _Float16*>(hidden), static_cast<const _Float16*>(hidden), T * topk, K, 0, 0,
+                  sorted_expert, perm_token, segs, nseg, static_cast<uint8_t*>(out), static_cast<_Float16*>(scales)};
+  return launch_act(false, a, T * topk + (with_shared ? T : 0), stream);
+}
+
+int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64_t T, int topk, int N, int N_shared,
+                             const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg, void* out,
+                             void* scales, void* stream) {
+  if (T < 0 || topk <= 0 || nseg <= 0 || N <= 0 || N % 128 || N > kMaxWidth ||
+      (shared_in && (N_shared <= 0 || N_shared % 128 || N_shared > kMaxWidth)))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_silu_mul_quant: widths must be multiples of 128 and <= %d (N=%d, "
+                "N_shared=%d)", kMaxWidth, N, N_shared);
+  if (T > 0 && (!routed_in || !sorted_expert || !segs || !out || !aligned16(routed_in) || !aligned16(out) ||
+                (shared_in && !aligned16(shared_in))))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_silu_mul_quant: NULL or misaligned pointer (16 B)");
+  const ActArgs a{static_cast<const _Float16*>(routed_in), static_cast<const _Float16*>(shared_in), T * topk, 0, N,
+                  N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
+                  static_cast<_Float16*>(scales)};
+  return launch_act(true, a, T * topk + (shared_in ? T : 0), stream);
+}
+
+int mxmoe_moe_combine(const void* y, const int32_t* inv_slot, const float* weights, const void* shared,
+                      const float* shared_w, int64_t T, int topk, int H, void* out, void* stream) {
+  if (T < 0 || topk <= 0 || H <= 0 || H % 8)
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_combine: need H %% 8 == 0, topk > 0 (H=%d)", H);
+  if (T == 0) return MXMOE_GG_OK;
+  if (!y || !inv_slot || !weights || !out || !aligned16(y) || !aligned16(out) || (shared && !aligned16(shared)))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_combine: NULL or misaligned pointer (16 B)");
+  hipLaunchKernelGGL(combine_kernel, dim3((unsigned)T), dim3(kThreads), 0, (hipStream_t)stream,
+                     static_cast<const _Float16*>(y), inv_slot, weights, static_cast<const _Float16*>(shared), shared_w,
+                     topk, H, static_cast<_Float16*>(out));
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "combine_kernel launch failed: %s", hipGetErrorString(e));
+  return MXMOE_GG_OK;
+}
+
+}  // extern "C"

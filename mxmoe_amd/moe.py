@@ -1,0 +1,351 @@
+"""MoE-layer plumbing around the GroupGEMM, on the C-ABI of include/mxmoe_moe.h.
+
+Reference interface mirrored (SeaCatComplexes/MxMoE, mxmoe/kernels/src/ref_bind.cu, pybind module
+``mxmoe_ops``):
+  * ``gg_permute_inp(hidden, topk_ids, E)`` ............................ ref_bind.cu:47-64
+  * ``quant_inp_act(hidden, topk_ids, num_experts, N, num_shared_experts, qparams_per_exp)``
+    -> (inp_list, inp_scale_list, out_list, inp_store, inp_scale_store, out_store,
+        recv_tokens_per_exp, perm_indices, dst_exp_sorted) .................. :434-592
+  * ``silu_mul_then_quant(inp, num_problems, num_experts, K, N, num_shared_experts, num_tokens, topk,
+    values_sorted, recv_tokens_per_exp, qparams_per_exp)``
+    -> (inp_list, inp_scale_list, out_list, inp_store, inp_scale_store, out_store) ... :595-757
+  * the per-expert quant tag ``cvt_qparams_to_tag`` ...................... :467-479
+  * ``gg_unpermute_out`` (an empty stub in the reference, :66) -> ``combine``
+and ``MoEFFN``: route -> quant_inp_act -> fused gate_up GroupGEMM -> silu_mul_then_quant -> fused
+down GroupGEMM -> combine, the layer the reference's ``gg_mxmoe_share_fused`` path builds toward.
+
+Differences by design: the routing is a device counting sort (mxmoe_moe_route) instead of
+torch::sort + bincount; the only host synchronisation is reading the per-expert token counts (the
+reference also moves them to the host: ``.cpu()`` at :456), which the tile planner needs anyway.
+The quantised activations are written in exactly the GroupGEMM operand layout: pack_wxax rows,
+per-token scales [rows] or, for w4a4 g128, [K/128][rows] (permute_scale layout).
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native as nat
+from .groupgemm import GroupGemm, Problem, QParams
+
+ACT_FP16, ACT_INT8, ACT_INT4, ACT_INT4_G128 = 0, 1, 2, 3
+_BITS = {ACT_FP16: 16, ACT_INT8: 8, ACT_INT4: 4, ACT_INT4_G128: 4}
+
+
+def qtag_of(a_bits: int, gsize: int) -> int:
+    """The reference's cvt_qparams_to_tag (ref_bind.cu:467-479); unsupported -> ValueError."""
+    if a_bits >= 16:
+        return ACT_FP16
+    if a_bits == 8 and gsize == -1:
+        return ACT_INT8
+    if a_bits == 4 and gsize == -1:
+        return ACT_INT4
+    if a_bits == 4 and gsize == 128:
+        return ACT_INT4_G128
+    raise ValueError(f"activation quantisation a{a_bits} g{gsize} not supported")
+
+
+def _stream(stream: Optional[torch.cuda.Stream]) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(int(s.cuda_stream))
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+@dataclasses.dataclass
+class Routing:
+    """Result of mxmoe_moe_route: slots sorted by expert (stable in token-major order)."""
+
+    sorted_expert: torch.Tensor  # int32 [T*topk] (the reference's values_sorted / dst_exp_sorted)
+    perm_token: torch.Tensor     # int32 [T*topk] (perm_indices)
+    inv_slot: torch.Tensor       # int32 [T*topk]: slot of (token t, choice k) at t*topk + k
+    counts: list[int]            # host copy of recv_tokens_per_exp [E]
+    T: int
+    topk: int
+    E: int
+
+    @property
+    def first_slot(self) -> list[int]:
+        out, acc = [], 0
+        for c in self.counts:
+            out.append(acc)
+            acc += c
+        return out
+
+
+def route(topk_ids: torch.Tensor, E: int, stream: Optional[torch.cuda.Stream] = None) -> Routing:
+    """Stable counting sort of the routing choices by expert (one HIP launch + the counts to host)."""
+    if topk_ids.dim() != 2:
+        raise ValueError("topk_ids must be [T, topk]")
+    T, topk = topk_ids.shape
+    dev = topk_ids.device
+    ids = topk_ids.to(torch.int32).contiguous()
+    n = T * topk
+    sorted_e = torch.empty(n, dtype=torch.int32, device=dev)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.zeros(E, dtype=torch.int32, device=dev)
+    nat.check(nat.lib().mxmoe_moe_route(_ptr(ids), T, topk, E, _ptr(sorted_e), _ptr(perm), _ptr(inv), _ptr(counts),
+                                        _stream(stream)))
+    c = counts.cpu().tolist()
+    if sum(c) != n:
+        raise ValueError(f"topk_ids holds {n - sum(c)} ids outside [0, {E})")
+    return Routing(sorted_e, perm, inv, c, T, topk, E)
+
+
+@dataclasses.dataclass
+class ActBatch:
+    """Permuted (and quantised) activations: one segment per expert (+ the shared expert)."""
+
+    out: torch.Tensor     # uint8 store of every segment's rows
+    scales: torch.Tensor  # fp16 store of every segment's scales
+    segs: list            # nat.MoeSegC per segment (host)
+    qtags: list[int]
+
+    def A(self, e: int) -> torch.Tensor:
+        """Segment e as the GroupGEMM A operand: fp16 [rows, width] or packed uint8 [rows, width*bits/8]."""
+        s = self.segs[e]
+        bits = _BITS[self.qtags[e]]
+        nbytes = s.rows * s.width * bits // 8
+        v = self.out[s.out_off:s.out_off + nbytes]
+        if bits == 16:
+            return v.view(torch.float16).view(max(s.rows, 0), s.width)
+        return v.view(s.rows, s.width * bits // 8)
+
+    def scale(self, e: int) -> Optional[torch.Tensor]:
+        s = self.segs[e]
+        tag = self.qtags[e]
+        if tag == ACT_FP16:
+            return None
+        n = s.rows * (s.width // 128 if tag == ACT_INT4_G128 else 1)
+        return self.scales[s.scale_off:s.scale_off + n]
+
+
+def _make_segments(rows: Sequence[int], first: Sequence[int], widths: Sequence[int], qtags: Sequence[int],
+                   device) -> tuple[list, torch.Tensor, torch.Tensor, torch.Tensor]:
+    segs, off, soff = [], 0, 0
+    for r, f, w, tag in zip(rows, first, widths, qtags):
+        if w % 128:
+            raise ValueError(f"segment width {w} must be a multiple of 128")
+        segs.append(nat.MoeSegC(tag, f, r, w, off, soff))
+        off += (r * w * _BITS[tag] // 8 + 15) // 16 * 16  # 16-B aligned A operands
+        soff += 0 if tag == ACT_FP16 else r * (w // 128 if tag == ACT_INT4_G128 else 1)
+    arr = (nat.MoeSegC * len(segs))(*segs)
+    dev_segs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+    out = torch.empty(max(off, 16), dtype=torch.uint8, device=device)
+    scales = torch.empty(max(soff, 1), dtype=torch.float16, device=device)
+    return segs, dev_segs, out, scales
+
+
+def quant_act(hidden: torch.Tensor, r: Routing, qtags: Sequence[int], with_shared: bool,
+              stream: Optional[torch.cuda.Stream] = None) -> ActBatch:
+    """Gather hidden rows into expert order and quantise each expert's rows by its tag
+    (len(qtags) == E, or E + 1 with the shared expert last)."""
+    T, K = hidden.shape
+    nseg = r.E + (1 if with_shared else 0)
+    if len(qtags) != nseg:
+        raise ValueError(f"need {nseg} quant tags, got {len(qtags)}")
+    rows = list(r.counts) + ([T] if with_shared else [])
+    first = r.first_slot + ([T * r.topk] if with_shared else [])
+    segs, dsegs, out, scales = _make_segments(rows, first, [K] * nseg, qtags, hidden.device)
+    h = hidden.contiguous()
+    nat.check(nat.lib().mxmoe_moe_quant_act(_ptr(h), T, K, r.topk, int(with_shared), _ptr(r.sorted_expert),
+                                            _ptr(r.perm_token), _ptr(dsegs), nseg, _ptr(out), _ptr(scales),
+                                            _stream(stream)))
+    b = ActBatch(out, scales, segs, list(qtags))
+    b._keep = (h, dsegs)  # the launch reads them asynchronously
+    return b
+
+
+def silu_mul_quant(routed: torch.Tensor, shared: Optional[torch.Tensor], r: Routing, qtags: Sequence[int],
+                   stream: Optional[torch.cuda.Stream] = None) -> ActBatch:
+    """act = silu(gate) * up of the gate_up outputs (routed [T*topk, 2N] in slot order, shared
+    [T, 2Ns]), quantised per expert for the down GroupGEMM."""
+    N = routed.shape[1] // 2
+    Ns = shared.shape[1] // 2 if shared is not None else 0
+    nseg = r.E + (1 if shared is not None else 0)
+    if len(qtags) != nseg:
+        raise ValueError(f"need {nseg} quant tags, got {len(qtags)}")
+    rows = list(r.counts) + ([r.T] if shared is not None else [])
+    first = r.first_slot + ([r.T * r.topk] if shared is not None else [])
+    widths = [N] * r.E + ([Ns] if shared is not None else [])
+    segs, dsegs, out, scales = _make_segments(rows, first, widths, qtags, routed.device)
+    nat.check(nat.lib().mxmoe_moe_silu_mul_quant(_ptr(routed), _ptr(shared), r.T, r.topk, N, Ns,
+                                                 _ptr(r.sorted_expert), _ptr(dsegs), nseg, _ptr(out), _ptr(scales),
+                                                 _stream(stream)))
+    b = ActBatch(out, scales, segs, list(qtags))
+    b._keep = (dsegs,)
+    return b
+
+
+def combine(y: torch.Tensor, r: Routing, weights: torch.Tensor, shared: Optional[torch.Tensor] = None,
+            shared_w: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """out[t] = sum_k weights[t,k] * y[slot(t,k)] (+ shared_w[t] * shared[t]), f32 fma chain, fp16 out."""
+    H = y.shape[1]
+    w = weights.to(torch.float32).contiguous()
+    sw = None if shared_w is None else shared_w.to(torch.float32).contiguous()
+    out = torch.empty(r.T, H, dtype=torch.float16, device=y.device)
+    nat.check(nat.lib().mxmoe_moe_combine(_ptr(y), _ptr(r.inv_slot), _ptr(w), _ptr(shared), _ptr(sw), r.T, r.topk, H,
+                                          _ptr(out), _stream(stream)))
+    return out
+
+
+# ------------------------------------------------------------------ reference-named entry points
+
+def _qtags(qparams_per_exp, n: int) -> list[int]:
+    return [qtag_of(int(q[0]), int(q[2])) for q in list(qparams_per_exp)[:n]]
+
+
+def gg_permute_inp(hidden: torch.Tensor, topk_ids: torch.Tensor, E: int):
+    """(num_problems, inp_buffer [T*topk, K] fp16 in expert order, indices, recv_tokens_per_exp)."""
+    r = route(topk_ids, E)
+    b = quant_act(hidden, r, [ACT_FP16] * E, with_shared=False)
+    T, K = hidden.shape
+    inp = b.out[: T * r.topk * K * 2].view(torch.float16).view(T * r.topk, K)
+    counts = torch.tensor(r.counts, dtype=torch.int64)
+    return sum(1 for c in r.counts if c), inp, r.perm_token.to(torch.int64), counts
+
+
+def quant_inp_act(hidden: torch.Tensor, topk_ids: torch.Tensor, num_experts: int, N: int, num_shared_experts: int,
+                  qparams_per_exp, verbose: bool = False):
+    """Mirror of ref_bind.cu:434-592. qparams_per_exp[e] = (a_bits, w_bits, gsize, sym), the shared
+    expert last. out_store / out_list: the gate_up output buffers (routed [T*topk, 2N] then
+    shared [T, 2N * num_shared_experts])."""
+    T = hidden.shape[0]
+    has_shared = num_shared_experts > 0
+    r = route(topk_ids, num_experts)
+    tags = _qtags(qparams_per_exp, num_experts + (1 if has_shared else 0))
+    b = quant_act(hidden, r, tags, has_shared)
+    out_store = torch.empty((num_shared_experts + r.topk) * T * N * 2, dtype=torch.float16, device=hidden.device)
+    inp_list, scale_list, out_list = [], [], []
+    off = 0
+    for e, s in enumerate(b.segs):
+        ld = 2 * N * (num_shared_experts if e == num_experts else 1)
+        if s.rows == 0:
+            continue
+        inp_list.append(b.A(e))
+        sc = b.scale(e)
+        scale_list.append(sc if sc is not None else torch.empty(0, dtype=torch.float16, device=hidden.device))
+        out_list.append(out_store[off:off + s.rows * ld].view(s.rows, ld))
+        off += s.rows * ld
+    if verbose:
+        print([(e, s.rows, s.qtag) for e, s in enumerate(b.segs)])
+    counts = torch.tensor(r.counts, dtype=torch.int64)
+    res = (inp_list, scale_list, out_list, b.out, b.scales, out_store, counts, r.perm_token.to(torch.int64),
+           r.sorted_expert)
+    return res
+
+
+def silu_mul_then_quant(inp: torch.Tensor, num_problems: int, num_experts: int, K: int, N: int,
+                        num_shared_experts: int, num_tokens: int, topk: int, values_sorted: torch.Tensor,
+                        recv_tokens_per_exp: torch.Tensor, qparams_per_exp):
+    """Mirror of ref_bind.cu:595-757: inp = the gate_up out_store (routed [T*topk, 2N] then shared
+    [T, 2N*S]); returns the quantised down-proj inputs and the down output store [(1+topk)*T*K]."""
+    T = num_tokens
+    S = num_shared_experts
+    routed = inp[: T * topk * 2 * N].view(T * topk, 2 * N)
+    shared = inp[T * topk * 2 * N: T * topk * 2 * N + T * 2 * N * S].view(T, 2 * N * S) if S > 0 else None
+    counts = [int(c) for c in recv_tokens_per_exp.tolist()]
+    r = Routing(values_sorted.to(torch.int32), torch.empty(0), torch.empty(0), counts, T, topk, num_experts)
+    tags = _qtags(qparams_per_exp, num_experts + (1 if S > 0 else 0))
+    b = silu_mul_quant(routed, shared, r, tags)
+    out_store = torch.empty((1 + topk) * T * K, dtype=torch.float16, device=inp.device)
+    inp_list, scale_list, out_list = [], [], []
+    off = 0
+    for e, s in enumerate(b.segs):
+        if s.rows == 0:
+            continue
+        inp_list.append(b.A(e))
+        sc = b.scale(e)
+        scale_list.append(sc if sc is not None else torch.empty(0, dtype=torch.float16, device=inp.device))
+        out_list.append(out_store[off:off + s.rows * K].view(s.rows, K))
+        off += s.rows * K
+    return inp_list, scale_list, out_list, b.out, b.scales, out_store
+
+
+# ------------------------------------------------------------------ the MoE FFN layer
+
+@dataclasses.dataclass
+class ExpertWeights:
+    """One linear's GroupGEMM B operand: fp16 [N, K] or packed codes + scale_b, and its QParams."""
+
+    B: torch.Tensor
+    scale_b: Optional[torch.Tensor]
+    q: QParams
+    N: int
+    K: int
+
+
+def prepare_weight(w: torch.Tensor, q: QParams) -> ExpertWeights:
+    """fp16 [N, K] -> the GroupGEMM's B operand for qcfg q (setup, once per weight)."""
+    from .quantize import pack_weightonly_mi355x, pack_wxax, quant_rtn_sym, quant_weightonly
+
+    N, K = w.shape
+    if not q.is_quant:
+        return ExpertWeights(w.contiguous(), None, q, N, K)
+    if q.is_weight_only:
+        codes, sz = quant_weightonly(w, q.w_bits, q.gsize, q.sym)
+        return ExpertWeights(pack_weightonly_mi355x(codes, q.w_bits), sz, q, N, K)
+    qw, sw = quant_rtn_sym(w, q.w_bits, q.gsize)
+    return ExpertWeights(pack_wxax(qw, q.w_bits), sw, q, N, K)
+
+
+class MoEFFN:
+    """A quantised MoE FFN layer (routed experts + optional shared expert) on the fused GroupGEMM.
+
+    gate_up[e]: fp16 [2N, H] (gate rows then up rows), down[e]: fp16 [H, N]; qcfg[e] = (QParams of
+    gate_up, QParams of down) — the activation side (a_bits, gsize) of each QParams sets how the
+    plumbing quantises that expert's input (qtag_of). Expert E (if given) is the shared expert."""
+
+    def __init__(self, gate_up: Sequence[torch.Tensor], down: Sequence[torch.Tensor],
+                 qcfg: Sequence[tuple[QParams, QParams]], num_routed: int):
+        self.E = num_routed
+        self.has_shared = len(gate_up) == num_routed + 1
+        self.H = gate_up[0].shape[1]
+        self.N = gate_up[0].shape[0] // 2
+        self.Ns = gate_up[-1].shape[0] // 2 if self.has_shared else 0
+        self.qcfg = list(qcfg)
+        self.w1 = [prepare_weight(w, q[0]) for w, q in zip(gate_up, qcfg)]
+        self.w2 = [prepare_weight(w, q[1]) for w, q in zip(down, qcfg)]
+        self.tag1 = [qtag_of(q[0].a_bits, q[0].gsize) for q in qcfg]
+        self.tag2 = [qtag_of(q[1].a_bits, q[1].gsize) for q in qcfg]
+
+    def forward(self, hidden: torch.Tensor, topk_ids: torch.Tensor, topk_weights: torch.Tensor,
+                shared_w: Optional[torch.Tensor] = None, return_intermediates: bool = False):
+        T = hidden.shape[0]
+        dev = hidden.device
+        r = route(topk_ids, self.E)
+        topk = r.topk
+        a1 = quant_act(hidden, r, self.tag1, self.has_shared)
+        h1 = torch.empty(T * topk, 2 * self.N, dtype=torch.float16, device=dev)
+        h1s = torch.empty(T, 2 * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
+        probs = []
+        for e, s in enumerate(a1.segs):
+            if s.rows == 0:
+                continue
+            w = self.w1[e]
+            C = h1s if e == self.E else h1[s.first_slot:s.first_slot + s.rows]
+            probs.append(Problem(A=a1.A(e), B=w.B, C=C, M=s.rows, N=w.N, K=w.K, q=w.q, scale_a=a1.scale(e),
+                                 scale_b=w.scale_b))
+        GroupGemm(probs, device=dev).launch()
+        a2 = silu_mul_quant(h1, h1s, r, self.tag2)
+        y = torch.empty(T * topk, self.H, dtype=torch.float16, device=dev)
+        ys = torch.empty(T, self.H, dtype=torch.float16, device=dev) if self.has_shared else None
+        probs = []
+        for e, s in enumerate(a2.segs):
+            if s.rows == 0:
+                continue
+            w = self.w2[e]
+            C = ys if e == self.E else y[s.first_slot:s.first_slot + s.rows]
+            probs.append(Problem(A=a2.A(e), B=w.B, C=C, M=s.rows, N=w.N, K=w.K, q=w.q, scale_a=a2.scale(e),
+                                 scale_b=w.scale_b))
+        GroupGemm(probs, device=dev).launch()
+        out = combine(y, r, topk_weights, ys, shared_w)
+        if return_intermediates:
+            return out, dict(routing=r, a1=a1, h1=h1, h1s=h1s, a2=a2, y=y, ys=ys)
+        return out
