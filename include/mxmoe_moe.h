@@ -67,7 +67,8 @@ int mxmoe_moe_quant_act(const void* hidden, int64_t T, int K, int topk, int with
                         const int32_t* sorted_expert, const int32_t* perm_token, const mxmoe_moe_seg* segs, int nseg,
                         void* out, void* scales, void* stream);
 
-/* act = fp16_rn(silu(f32 g) * f32 u) of the gate_up output, then quantised as mxmoe_moe_quant_act.
+/* act = fp16_rn(silu(f32 g) * f32 u) of the gate_up output (silu(g) = g * rcp(1 + exp2(-g log2 e)) with
+ * the hardware exp2 / reciprocal), then quantised as mxmoe_moe_quant_act.
  * routed_in: fp16 [T*topk][2*N] (slot order; gate = columns [0, N), up = [N, 2N));
  * shared_in: fp16 [T][2*N_shared] or NULL (non-NULL: slots T*topk + t, segment nseg - 1). Segment widths: N for routed experts,
  * N_shared for the shared one (both multiples of 128, <= 16384). */

@@ -152,7 +152,7 @@ Variant make_v2(const char* name) {
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 128, 512};
   v.geom[QT_W4A16] = {256, 256, 32, 512};  // 64-K stages: 32 B of 4-bit codes per row
   v.geom[QT_W8A16] = {256, 256, 64, 512};
-  v.geom[QT_I4G] = {128, 256, 128, 512};  // w4a4 g128: 128-row tiles only (gg_tile_g128)
+  v.geom[QT_I4G] = {256, 256, 128, 512};  // w4a4 g128 (gg_tile_g128): 256 / 128-row classes as int4
   v.threads = 512;
   v.lds_bytes = V2Cfg<256>::LDS_BYTES;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
@@ -390,10 +390,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
       const bool small_class = m.qtype == QT_F16 || m.qtype == QT_W4A16 || m.qtype == QT_W8A16;
-      if (m.qtype == QT_I4G) {  // one 128-row tile body (class 1) for every m-tile
-        mt.push_back({m0, 1});
-        m0 += g.bm;
-      } else if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
+      if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
         mt.push_back({m0, 2});
         m0 += v.tail2_bm;
       } else if (v.kind != Kind::V0 && v.tail_bm && rem <= v.tail_bm) {

@@ -386,6 +386,10 @@ struct V2Cfg {
   static_assert(WTN == 64, "epilogue assumes 128-B staged rows");
 };
 
+// LDS beyond the two 128-KiB-image stages: the int paths' tile scales (1 KiB) and the w4a4 g128
+// group-scale slots (2 x 2 KiB after a 256-row tile's two stages)
+constexpr int V2_LDS_EXTRA = 4096;
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
@@ -841,7 +845,7 @@ __device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __
   static_assert(Cfg::BM <= 256 && Cfg::BN == 256, "scale slot holds 256 rows / columns per group");
   constexpr int SCL = 2 * Cfg::STAGE_BYTES;  // LDS scale slots: [buf][sa 2 x 256 | sb 2 x 256] fp16
   constexpr int SCL_BYTES = 2048;
-  static_assert(SCL + 2 * SCL_BYTES <= V2Cfg<256>::LDS_BYTES, "scale slots must fit the v2 LDS image");
+  static_assert(SCL + 2 * SCL_BYTES <= V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA, "scale slots must fit the v2 LDS image");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
@@ -889,28 +893,32 @@ __device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __
       }
     }
   };
-  // group scales of stage s: threads 0-255 one sa value (group tid >> 7, row tid & 127 — BM <= 128
-  // rows used), threads 256-511 the two sb values of column tid - 256
+  // group scales of stage s (groups 2s, 2s+1), two halves per thread: threads 0-255 the sa of tile
+  // row tid (rows < BM), threads 256-511 the sb of tile column tid - 256
   uint32_t sc = 0;
   auto load_scales = [&](int s) {
     const int g0 = 2 * s;
+    const bool two = g0 + 1 < ngroups;
     if (tid < 256) {
-      const int gg = g0 + (tid >> 7), r = tid & 127;
-      if (gg < ngroups && r < Cfg::BM) sc = __builtin_bit_cast(uint16_t, SA[(int64_t)gg * M + min(m0 + r, M - 1)]);
+      if (tid < Cfg::BM) {
+        const int64_t r = min(m0 + tid, M - 1);
+        const uint32_t lo = __builtin_bit_cast(uint16_t, SA[(int64_t)g0 * M + r]);
+        const uint32_t hi = two ? __builtin_bit_cast(uint16_t, SA[(int64_t)(g0 + 1) * M + r]) : 0u;
+        sc = lo | (hi << 16);
+      }
     } else {
-      const int n = min(n0 + tid - 256, N - 1);
+      const int64_t n = min(n0 + tid - 256, N - 1);
       const uint32_t lo = __builtin_bit_cast(uint16_t, SB[(int64_t)g0 * N + n]);
-      const uint32_t hi = g0 + 1 < ngroups ? __builtin_bit_cast(uint16_t, SB[(int64_t)(g0 + 1) * N + n]) : 0u;
+      const uint32_t hi = two ? __builtin_bit_cast(uint16_t, SB[(int64_t)(g0 + 1) * N + n]) : 0u;
       sc = lo | (hi << 16);
     }
   };
   auto stash_scales = [&](int buf) {
     uint16_t* sl = reinterpret_cast<uint16_t*>(lds + SCL + buf * SCL_BYTES);
-    if (tid < 256) {
-      sl[(tid >> 7) * 256 + (tid & 127)] = (uint16_t)sc;
-    } else {
-      sl[512 + tid - 256] = (uint16_t)sc;
-      sl[768 + tid - 256] = (uint16_t)(sc >> 16);
+    if (tid >= 256 || tid < Cfg::BM) {
+      const int c = tid < 256 ? tid : 512 + tid - 256;
+      sl[c] = (uint16_t)sc;
+      sl[c + 256] = (uint16_t)(sc >> 16);
     }
   };
 
@@ -923,6 +931,23 @@ __device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __
   const int swz = (r16 >> 1) & 7;
   const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
+  // fold of fragment row i: out += f32(acc) * f32(fp16_rn(sa * sb)), one rounding (v_fma_mix_f32)
+  auto fold = [&](int i, const v4i (&acc)[FN], const uint2 (&sbw)[FN], _Float16 sai) {
+    const h2_t sa2 = {sai, sai};
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const uint32_t s01 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw[j].x));
+      const uint32_t s23 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw[j].y));
+      out[i][j][0] = fma_f32_f16lo((float)acc[j][0], s01, out[i][j][0]);
+      out[i][j][1] = fma_f32_f16hi((float)acc[j][1], s01, out[i][j][1]);
+      out[i][j][2] = fma_f32_f16lo((float)acc[j][2], s23, out[i][j][2]);
+      out[i][j][3] = fma_f32_f16hi((float)acc[j][3], s23, out[i][j][3]);
+    }
+  };
+  // one group = two 64-element MFMA steps. Row-pipelined: the group's B fragments (both steps)
+  // stay in registers, fragment row i's int32 accumulators are formed by 2 * FN MFMAs and folded
+  // while row i+1's MFMAs run (two accumulator sets) — the fold's VALU sits beside the matrix
+  // pipe's work instead of after all of it, and only 2 * FN int32 fragments are ever live.
   auto compute = [&](int buf, int s) {
     const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
     const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
@@ -930,42 +955,32 @@ __device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h == 1 && 2 * s + 1 >= ngroups) break;  // K tail: no second group in this stage
-      v4i acc[FM][FN];
+      const uint32_t off0 = (uint32_t)(((4 * h + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
+      const uint32_t off1 = (uint32_t)(((4 * h + 2 + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
+      v4i b0[FN], b1[FN];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int st = 2 * h + t;
-        const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
-        v4i a[FM], b[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off));
-#pragma unroll
-        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off));
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], t == 0 ? v4i{0, 0, 0, 0} : acc[i][j], 0, 0, 0);
+      for (int j = 0; j < FN; ++j) {
+        b0[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off0));
+        b1[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off1));
       }
-      // fold: out += f32(acc) * f32(fp16_rn(sa * sb)) with one rounding (v_fma_mix_f32)
-      const _Float16* sa = sl + h * 256 + wm * Cfg::WTM + r16;
       const uint2* sbp = reinterpret_cast<const uint2*>(sl + 512 + h * 256 + wn * Cfg::WTN + 4 * g);
       uint2 sbw[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) sbw[j] = sbp[j * 4];
+      const _Float16* sa = sl + h * 256 + wm * Cfg::WTM + r16;
+      v4i acc0[FN], acc1[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const _Float16 sai = sa[i * 16];
-        const h2_t sa2 = {sai, sai};
+        v4i (&acc)[FN] = (i & 1) ? acc1 : acc0;
+        const v4i a0 = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off0));
+        const v4i a1 = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off1));
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const uint32_t s01 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw[j].x));
-          const uint32_t s23 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw[j].y));
-          out[i][j][0] = fma_f32_f16lo((float)acc[i][j][0], s01, out[i][j][0]);
-          out[i][j][1] = fma_f32_f16hi((float)acc[i][j][1], s01, out[i][j][1]);
-          out[i][j][2] = fma_f32_f16lo((float)acc[i][j][2], s23, out[i][j][2]);
-          out[i][j][3] = fma_f32_f16hi((float)acc[i][j][3], s23, out[i][j][3]);
-        }
+        for (int j = 0; j < FN; ++j) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b0[j], a0, v4i{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b1[j], a1, acc[j], 0, 0, 0);
+        if (i > 0) fold(i - 1, (i & 1) ? acc0 : acc1, sbw, sa[(i - 1) * 16]);
       }
+      fold(FM - 1, ((FM - 1) & 1) ? acc1 : acc0, sbw, sa[(FM - 1) * 16]);
     }
   };
 
@@ -986,21 +1001,26 @@ __device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __
   }
 
   // ---- epilogue (as gg_tile_v2): out * 2^-8 (exact) -> fp16, per-wave LDS staging, 16-B stores ----
+  // (lane indices re-derived from an opaque copy of threadIdx.x: keeping the mainloop's copies live
+  // across the K loop cost the 256-row body a VGPR spill)
+  int etid = threadIdx.x;
+  asm volatile("" : "+v"(etid));
+  const int elane = etid & 63, er16 = elane & 15, eg = elane >> 4;
   uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
   const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int ml = i * 16 + r16;
+    const int ml = i * 16 + er16;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const uint2 pk = pack4_f16(out[i][j] * (1.0f / 256.0f));
-      const int q = 2 * j + (g >> 1);
-      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
+      const int q = 2 * j + (eg >> 1);
+      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (eg & 1) * 8) = pk;
     }
   }
 #pragma unroll 4
   for (int it = 0; it < Cfg::WTM / 8; ++it) {
-    const int row = it * 8 + (lane >> 3), q = lane & 7;
+    const int row = it * 8 + (elane >> 3), q = elane & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
     const int m = mrow0 + row, n = ncol0 + q * 8;
     if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
@@ -1473,7 +1493,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
 __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   // + the int paths' scale stash: SA at [LDS_BYTES, +2*BM), SB at [LDS_BYTES + 512, +512)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES + 1024];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA];
   if constexpr ((ABL & V2_TRACE) != 0) trace_mark(0);
   const TileDesc td = args.tiles[blockIdx.x];
   if (td.prob < 0) return;
@@ -1504,7 +1524,8 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v2<V2Cfg<128>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);  // no 64-row class
   } else if ((QM & (1 << QT_I4G)) && mt.qtype == QT_I4G) {
-    gg_tile_g128<V2Cfg<128>>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);  // 128-row tiles only
+    if (cls == 0) gg_tile_g128<V2Cfg<256>>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_g128<V2Cfg<128>>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);

@@ -38,6 +38,7 @@ int fail(int code, const char* fmt, ...) {
 }
 
 constexpr int kThreads = 256;
+constexpr int kRouteThreads = 1024;
 constexpr int kChunk = kThreads * 8;     // fp16 elements one pass of the workgroup covers
 constexpr int kMaxChunks = 8;            // rows up to 16384 elements
 constexpr int kMaxWidth = kChunk * kMaxChunks;
@@ -54,7 +55,8 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-// exclusive block prefix of v (256 threads) and the block total
+// exclusive block prefix of v (NT threads) and the block total
+template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int* total, int* lds4) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int incl = wave_incl_scan(v);
@@ -62,7 +64,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* total, int* lds4) {
   __syncthreads();
   int base = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kThreads / 64; ++w) {
+  for (int w = 0; w < NT / 64; ++w) {
     base += w < wave ? lds4[w] : 0;
     tot += lds4[w];
   }
@@ -71,47 +73,54 @@ __device__ __forceinline__ int block_excl_scan(int v, int* total, int* lds4) {
   return base + incl - v;
 }
 
-__device__ __forceinline__ float block_max(float v, float* lds4) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
-  if (lane == 0) lds4[wave] = v;
-  __syncthreads();
-  float m = lds4[0];
-#pragma unroll
-  for (int w = 1; w < kThreads / 64; ++w) m = fmaxf(m, lds4[w]);
-  return m;
-}
-
 // ---------------------------------------------------------------------------------------------
 // route: workgroup e finds every id == e in flattened order (stable), its slot base = #ids < e.
 // Each thread scans a contiguous run of the ids twice (count, then place); the runs' counts are
 // prefix-summed across the workgroup so the placement keeps the flattened order.
-__global__ __launch_bounds__(kThreads) void route_kernel(const int32_t* __restrict__ ids, int n, int topk,
-                                                         int32_t* __restrict__ sorted, int32_t* __restrict__ perm,
-                                                         int32_t* __restrict__ inv, int32_t* __restrict__ counts) {
-  __shared__ int lds4[kThreads / 64];
+__global__ __launch_bounds__(kRouteThreads) void route_kernel(const int32_t* __restrict__ ids, int n, int topk,
+                                                              int32_t* __restrict__ sorted, int32_t* __restrict__ perm,
+                                                              int32_t* __restrict__ inv, int32_t* __restrict__ counts) {
+  __shared__ int lds[kRouteThreads / 64];
   const int e = blockIdx.x;
-  const int per = (n + kThreads - 1) / kThreads;
-  const int b = threadIdx.x * per, end = min(n, b + per);
+  // run of 4*q ids per thread (q int4 words, read as independent 16-B loads); ids past n read as -1
+  const int q = (n + 4 * kRouteThreads - 1) / (4 * kRouteThreads);
+  const int b = threadIdx.x * q * 4;
+  auto id4 = [&](int w) -> int4 {
+    const int i = b + 4 * w;
+    if (i + 4 <= n && (n & 3) == 0) return *reinterpret_cast<const int4*>(ids + i);
+    int4 v;
+    v.x = i < n ? ids[i] : -1;
+    v.y = i + 1 < n ? ids[i + 1] : -1;
+    v.z = i + 2 < n ? ids[i + 2] : -1;
+    v.w = i + 3 < n ? ids[i + 3] : -1;
+    return v;
+  };
   int less = 0, eq = 0;
-  for (int i = b; i < end; ++i) {
-    const int v = ids[i];
-    less += (v >= 0 && v < e);
-    eq += v == e;
+#pragma unroll 8
+  for (int w = 0; w < q; ++w) {
+    const int4 v = id4(w);
+    less += (v.x >= 0 && v.x < e) + (v.y >= 0 && v.y < e) + (v.z >= 0 && v.z < e) + (v.w >= 0 && v.w < e);
+    eq += (v.x == e) + (v.y == e) + (v.z == e) + (v.w == e);
   }
   int eq_total, less_total;
-  const int rank = block_excl_scan(eq, &eq_total, lds4);
-  block_excl_scan(less, &less_total, lds4);
+  const int rank = block_excl_scan<kRouteThreads>(eq, &eq_total, lds);
+  block_excl_scan<kRouteThreads>(less, &less_total, lds);
   if (threadIdx.x == 0) counts[e] = eq_total;
+  if (eq == 0) return;
   int pos = less_total + rank;
-  for (int i = b; i < end && eq > 0; ++i) {
-    if (ids[i] == e) {
-      sorted[pos] = e;
-      perm[pos] = i / topk;
-      inv[i] = pos;
-      ++pos;
-      --eq;
+  for (int w = 0; w < q && eq > 0; ++w) {
+    const int4 v = id4(w);
+    const int vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (vv[j] == e) {
+        const int i = b + 4 * w + j;
+        sorted[pos] = e;
+        perm[pos] = i / topk;
+        inv[i] = pos;
+        ++pos;
+        --eq;
+      }
     }
   }
 }
@@ -121,6 +130,8 @@ struct ActArgs {
   const _Float16* src;         // quant: hidden [T][K]; silu: routed gate_up [T*topk][2N]
   const _Float16* src_shared;  // silu: shared gate_up [T][2Ns] (quant: = src)
   int64_t ntk;                 // T * topk routed slots
+  int64_t nslots;              // end of the launch's slot range (ntk, + T shared slots)
+  int64_t s0;                  // first slot of the launch
   int K;                       // quant: row width of hidden
   int N, Ns;                   // silu: routed / shared intermediate width
   const int32_t* sorted;
@@ -156,11 +167,15 @@ __device__ __forceinline__ int rtn_code(_Float16 x, _Float16 s, float qmax) {
   return (int)__builtin_rintf(d);
 }
 
-template <bool SILU>
+// One WAVE per slot row (4 rows per 256-thread workgroup): lane l holds elements c*512 + 8l .. +7
+// of chunk c in registers (MAXC chunks: rows up to MAXC*512 elements), so every lane has MAXC
+// independent 16-B loads in flight, the per-token amax is a wave butterfly and a 128-element group
+// is 16 adjacent lanes — no LDS, no barrier.
+template <bool SILU, int MAXC>
 __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
-  __shared__ float lds4[kThreads / 64];
-  const int64_t s = blockIdx.x;
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = a.s0 + (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (s >= a.nslots) return;
   int e;
   const _Float16* row_src;
   if (s < a.ntk) {
@@ -178,32 +193,37 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const int width = sg.width;
   const int upoff = SILU ? (s < a.ntk ? a.N : a.Ns) : 0;  // column of the "up" half
 
-  h8_t x[kMaxChunks];
+  // every load of the row first (all in flight together), then the arithmetic
+  h8_t x[MAXC];
+  h8_t u[SILU ? MAXC : 1];
 #pragma unroll
-  for (int c = 0; c < kMaxChunks; ++c) {
-    const int idx = c * kChunk + tid * 8;
+  for (int c = 0; c < MAXC; ++c) {
+    const int idx = c * 512 + lane * 8;
+    x[c] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (SILU) u[c] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
     if (idx < width) {
-      if constexpr (SILU) {
-        const h8_t gv = *reinterpret_cast<const h8_t*>(row_src + idx);
-        const h8_t uv = *reinterpret_cast<const h8_t*>(row_src + upoff + idx);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float g = (float)gv[j];
-          x[c][j] = (_Float16)((g / (1.0f + expf(-g))) * (float)uv[j]);
-        }
-      } else {
-        x[c] = *reinterpret_cast<const h8_t*>(row_src + idx);
-      }
-    } else {
-      x[c] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      x[c] = *reinterpret_cast<const h8_t*>(row_src + idx);
+      if constexpr (SILU) u[c] = *reinterpret_cast<const h8_t*>(row_src + upoff + idx);
     }
+  }
+  if constexpr (SILU) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // silu(g) = g / (1 + e^-g) with the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: the
+        // reference kernel is absent, so this is our definition; oracle/moe_ref.py allows 1 ulp)
+        const float g = (float)x[c][j];
+        const float sg = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g * -1.4426950408889634f));
+        x[c][j] = (_Float16)(sg * (float)u[c][j]);
+      }
   }
 
   if (sg.qtag == MXMOE_ACT_FP16) {
     _Float16* o = reinterpret_cast<_Float16*>(a.out + sg.out_off) + row * width;
 #pragma unroll
-    for (int c = 0; c < kMaxChunks; ++c) {
-      const int idx = c * kChunk + tid * 8;
+    for (int c = 0; c < MAXC; ++c) {
+      const int idx = c * 512 + lane * 8;
       if (idx < width) *reinterpret_cast<h8_t*>(o + idx) = x[c];
     }
     return;
@@ -212,11 +232,10 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const float qmax = bits == 8 ? 127.0f : 7.0f;
   uint8_t* o = a.out + sg.out_off + row * (int64_t)width * bits / 8;
   if (sg.qtag == MXMOE_ACT_INT4_G128) {
-    // 16 consecutive lanes hold one 128-element group of a chunk
 #pragma unroll
-    for (int c = 0; c < kMaxChunks; ++c) {
-      const int idx = c * kChunk + tid * 8;
-      if (c * kChunk >= width) break;  // uniform
+    for (int c = 0; c < MAXC; ++c) {
+      if (c * 512 >= width) break;  // uniform
+      const int idx = c * 512 + lane * 8;
       float m = 0.0f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)x[c][j]));
@@ -228,22 +247,23 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, qmax);
         *reinterpret_cast<uint32_t*>(o + idx / 2) = pack_i4x8(q);
-        if ((tid & 15) == 0) a.scales[sg.scale_off + (int64_t)(idx / 128) * sg.rows + row] = sc;
+        if ((lane & 15) == 0) a.scales[sg.scale_off + (int64_t)(idx / 128) * sg.rows + row] = sc;
       }
     }
     return;
   }
   float m = 0.0f;
 #pragma unroll
-  for (int c = 0; c < kMaxChunks; ++c)
+  for (int c = 0; c < MAXC; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)x[c][j]));
-  m = block_max(m, lds4);
-  const _Float16 sc = rtn_scale(m, qmax);
-  if (tid == 0) a.scales[sg.scale_off + row] = sc;
 #pragma unroll
-  for (int c = 0; c < kMaxChunks; ++c) {
-    const int idx = c * kChunk + tid * 8;
+  for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  const _Float16 sc = rtn_scale(m, qmax);
+  if (lane == 0) a.scales[sg.scale_off + row] = sc;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int idx = c * 512 + lane * 8;
     if (idx >= width) continue;
     int q[8];
 #pragma unroll
@@ -292,6 +312,36 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 using namespace mxmoe;
 
+template <bool SILU>
+static void launch_act_w(const ActArgs& a, int maxw, hipStream_t st) {
+  const dim3 grid((unsigned)((a.nslots - a.s0 + kThreads / 64 - 1) / (kThreads / 64))), block(kThreads);
+  if (maxw <= 2048) hipLaunchKernelGGL((act_quant_kernel<SILU, 4>), grid, block, 0, st, a);
+  else if (maxw <= 4096) hipLaunchKernelGGL((act_quant_kernel<SILU, 8>), grid, block, 0, st, a);
+  else if (maxw <= 8192) hipLaunchKernelGGL((act_quant_kernel<SILU, 16>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((act_quant_kernel<SILU, 32>), grid, block, 0, st, a);
+}
+
+// slots [0, nslots): one launch, or (rows of different widths) routed slots [0, ntk) and shared
+// slots [ntk, nslots) as two launches, each with the register row of its own width
+static int launch_act(bool silu, ActArgs a, int64_t nslots, int w_routed, int w_shared, void* stream) {
+  if (nslots == 0) return MXMOE_GG_OK;
+  const bool split = nslots > a.ntk && w_routed != w_shared && a.ntk > 0;
+  a.s0 = 0;
+  a.nslots = split ? a.ntk : nslots;
+  const int w0 = split ? w_routed : (nslots > a.ntk ? (w_routed > w_shared ? w_routed : w_shared) : w_routed);
+  if (silu) launch_act_w<true>(a, w0, (hipStream_t)stream);
+  else launch_act_w<false>(a, w0, (hipStream_t)stream);
+  if (split) {
+    a.s0 = a.ntk;
+    a.nslots = nslots;
+    if (silu) launch_act_w<true>(a, w_shared, (hipStream_t)stream);
+    else launch_act_w<false>(a, w_shared, (hipStream_t)stream);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "act_quant_kernel launch failed: %s", hipGetErrorString(e));
+  return MXMOE_GG_OK;
+}
+
 extern "C" {
 
 int mxmoe_moe_route(const int32_t* topk_ids, int64_t T, int topk, int E, int32_t* sorted_expert,
@@ -301,19 +351,10 @@ int mxmoe_moe_route(const int32_t* topk_ids, int64_t T, int topk, int E, int32_t
   if (T > 0 && (!topk_ids || !sorted_expert || !perm_token || !inv_slot))
     return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_route: NULL pointer");
   if (!counts) return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_route: NULL counts");
-  hipLaunchKernelGGL(route_kernel, dim3(E), dim3(kThreads), 0, (hipStream_t)stream, topk_ids, (int)(T * topk), topk,
+  hipLaunchKernelGGL(route_kernel, dim3(E), dim3(kRouteThreads), 0, (hipStream_t)stream, topk_ids, (int)(T * topk), topk,
                      sorted_expert, perm_token, inv_slot, counts);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "route_kernel launch failed: %s", hipGetErrorString(e));
-  return MXMOE_GG_OK;
-}
-
-static int launch_act(bool silu, const ActArgs& a, int64_t nslots, void* stream) {
-  if (nslots == 0) return MXMOE_GG_OK;
-  if (silu) hipLaunchKernelGGL(act_quant_kernel<true>, dim3((unsigned)nslots), dim3(kThreads), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(act_quant_kernel<false>, dim3((unsigned)nslots), dim3(kThreads), 0, (hipStream_t)stream, a);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "act_quant_kernel launch failed: %s", hipGetErrorString(e));
   return MXMOE_GG_OK;
 }
 
@@ -325,9 +366,9 @@ int mxmoe_moe_quant_act(const void* hidden, int64_t T, int K, int topk, int with
                 kMaxWidth, K);
   if (T > 0 && (!hidden || !sorted_expert || !perm_token || !segs || !out || !aligned16(hidden) || !aligned16(out)))
     return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_quant_act: NULL or misaligned pointer (hidden / out need 16 B)");
-  const ActArgs a{static_cast<const _Float16*>(hidden), static_cast<const _Float16*>(hidden), T * topk, K, 0, 0,
+  const ActArgs a{static_cast<const _Float16*>(hidden), static_cast<const _Float16*>(hidden), T * topk, 0, 0, K, 0, 0,
                   sorted_expert, perm_token, segs, nseg, static_cast<uint8_t*>(out), static_cast<_Float16*>(scales)};
-  return launch_act(false, a, T * topk + (with_shared ? T : 0), stream);
+  return launch_act(false, a, T * topk + (with_shared ? T : 0), K, K, stream);
 }
 
 int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64_t T, int topk, int N, int N_shared,
@@ -340,10 +381,10 @@ int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64
   if (T > 0 && (!routed_in || !sorted_expert || !segs || !out || !aligned16(routed_in) || !aligned16(out) ||
                 (shared_in && !aligned16(shared_in))))
     return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_silu_mul_quant: NULL or misaligned pointer (16 B)");
-  const ActArgs a{static_cast<const _Float16*>(routed_in), static_cast<const _Float16*>(shared_in), T * topk, 0, N,
-                  N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
+  const ActArgs a{static_cast<const _Float16*>(routed_in), static_cast<const _Float16*>(shared_in), T * topk, 0, 0, 0,
+                  N, N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
                   static_cast<_Float16*>(scales)};
-  return launch_act(true, a, T * topk + (shared_in ? T : 0), stream);
+  return launch_act(true, a, T * topk + (shared_in ? T : 0), N, shared_in ? N_shared : N, stream);
 }
 
 int mxmoe_moe_combine(const void* y, const int32_t* inv_slot, const float* weights, const void* shared,

@@ -78,20 +78,28 @@ class Routing:
         return out
 
 
+def route_device(topk_ids: torch.Tensor, E: int, stream: Optional[torch.cuda.Stream] = None, out=None):
+    """The routing launch alone (no host synchronisation): (sorted_expert, perm_token, inv_slot, counts)
+    device int32 tensors; `out` reuses a previous result's buffers."""
+    if topk_ids.dim() != 2 or topk_ids.dtype != torch.int32 or not topk_ids.is_contiguous():
+        raise ValueError("topk_ids must be a contiguous int32 [T, topk] tensor")
+    T, topk = topk_ids.shape
+    dev = topk_ids.device
+    n = T * topk
+    if out is None:
+        out = tuple(torch.empty(n, dtype=torch.int32, device=dev) for _ in range(3)) + (
+            torch.empty(E, dtype=torch.int32, device=dev),)
+    nat.check(nat.lib().mxmoe_moe_route(_ptr(topk_ids), T, topk, E, *(_ptr(t) for t in out), _stream(stream)))
+    return out
+
+
 def route(topk_ids: torch.Tensor, E: int, stream: Optional[torch.cuda.Stream] = None) -> Routing:
     """Stable counting sort of the routing choices by expert (one HIP launch + the counts to host)."""
     if topk_ids.dim() != 2:
         raise ValueError("topk_ids must be [T, topk]")
     T, topk = topk_ids.shape
-    dev = topk_ids.device
-    ids = topk_ids.to(torch.int32).contiguous()
     n = T * topk
-    sorted_e = torch.empty(n, dtype=torch.int32, device=dev)
-    perm = torch.empty(n, dtype=torch.int32, device=dev)
-    inv = torch.empty(n, dtype=torch.int32, device=dev)
-    counts = torch.zeros(E, dtype=torch.int32, device=dev)
-    nat.check(nat.lib().mxmoe_moe_route(_ptr(ids), T, topk, E, _ptr(sorted_e), _ptr(perm), _ptr(inv), _ptr(counts),
-                                        _stream(stream)))
+    sorted_e, perm, inv, counts = route_device(topk_ids.to(torch.int32).contiguous(), E, stream)
     c = counts.cpu().tolist()
     if sum(c) != n:
         raise ValueError(f"topk_ids holds {n - sum(c)} ids outside [0, {E})")
@@ -154,11 +162,15 @@ def quant_act(hidden: torch.Tensor, r: Routing, qtags: Sequence[int], with_share
     first = r.first_slot + ([T * r.topk] if with_shared else [])
     segs, dsegs, out, scales = _make_segments(rows, first, [K] * nseg, qtags, hidden.device)
     h = hidden.contiguous()
-    nat.check(nat.lib().mxmoe_moe_quant_act(_ptr(h), T, K, r.topk, int(with_shared), _ptr(r.sorted_expert),
-                                            _ptr(r.perm_token), _ptr(dsegs), nseg, _ptr(out), _ptr(scales),
-                                            _stream(stream)))
+
+    def launch(st=stream):
+        nat.check(nat.lib().mxmoe_moe_quant_act(_ptr(h), T, K, r.topk, int(with_shared), _ptr(r.sorted_expert),
+                                                _ptr(r.perm_token), _ptr(dsegs), nseg, _ptr(out), _ptr(scales),
+                                                _stream(st)))
+
+    launch()
     b = ActBatch(out, scales, segs, list(qtags))
-    b._keep = (h, dsegs)  # the launch reads them asynchronously
+    b.relaunch = launch  # same buffers, kernel only (timing / graph capture); keeps h and dsegs alive
     return b
 
 
@@ -175,11 +187,14 @@ def silu_mul_quant(routed: torch.Tensor, shared: Optional[torch.Tensor], r: Rout
     first = r.first_slot + ([r.T * r.topk] if shared is not None else [])
     widths = [N] * r.E + ([Ns] if shared is not None else [])
     segs, dsegs, out, scales = _make_segments(rows, first, widths, qtags, routed.device)
-    nat.check(nat.lib().mxmoe_moe_silu_mul_quant(_ptr(routed), _ptr(shared), r.T, r.topk, N, Ns,
-                                                 _ptr(r.sorted_expert), _ptr(dsegs), nseg, _ptr(out), _ptr(scales),
-                                                 _stream(stream)))
+    def launch(st=stream):
+        nat.check(nat.lib().mxmoe_moe_silu_mul_quant(_ptr(routed), _ptr(shared), r.T, r.topk, N, Ns,
+                                                     _ptr(r.sorted_expert), _ptr(dsegs), nseg, _ptr(out),
+                                                     _ptr(scales), _stream(st)))
+
+    launch()
     b = ActBatch(out, scales, segs, list(qtags))
-    b._keep = (dsegs,)
+    b.relaunch = launch
     return b
 
 

@@ -9,8 +9,9 @@ Only tests/ may import this module, as the checker. It restates, in numpy + the 
                       and packed by pack_wxax (quantize.cuh:425-475)
   silu_mul .......... act = fp16(f32(silu(f32 g)) * f32 u): the reference's silu_mul_then_quant_kernel
                       lives in the missing act_kernel.cuh, so this arithmetic is "parity unpinned"
-                      (our definition; exp is libm's expf here and ocml's on the GPU: up to 1 ulp apart,
-                      which the tests tolerate)
+                      (our definition; exp is libm's expf here, the GPU uses the hardware v_exp_f32 /
+                      v_rcp_f32 approximations: a few f32 ulps apart, i.e. at most 1 fp16 ulp / 1 code
+                      step after rounding, which the tests tolerate)
   combine ........... acc = fma(w_k, y_k, acc) over k in order, then fma(shared_w, shared, acc), fp16
                       (gg_unpermute_out is an empty stub in the reference, :66: our definition)
 """

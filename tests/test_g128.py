@@ -91,7 +91,7 @@ def test_planner_accepts_g128_and_rejects_bad_shapes():
 
 def test_variant_listing_names_g128():
     lines = [ln for ln in nat.list_variants() if ln.split()[1].startswith("v2s")]
-    assert any("w4a4_g128_sym=TileConfig(BM=128, BN=256, BK=256" in ln for ln in lines)
+    assert any("w4a4_g128_sym=TileConfig(BM=256, BN=256, BK=256" in ln for ln in lines)
 
 
 # ------------------------------------------------------------------------------------------ GPU
