@@ -813,9 +813,10 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 // (`frag_out += T(acc) * T(sa * sb)`, mm_tile.cuh:490-493, which nvcc contracts to one FFMA).
 // Scales: fp16 [K/128][M] and [K/128][N] (permute_scale, quantize.cuh:299-315; test.cu:283-313).
 //
-// MI355X layout: the 128-row v2 tile (8 waves 2M x 4N, wave tile 64 x 64) — the int32 group
-// accumulators and the f32 fold accumulators both live in registers, which a 128 x 64 wave tile
-// would not fit. One 128-B K stage = 256 int4 = two groups: MFMA steps 0-1 form group 2s, steps
+// MI355X layout: the v2 tiles (8 waves 2M x 4N; 256-row class with 128 x 64 wave tiles, 128-row
+// class for a problem's last rows). The f32 fold accumulators live in registers for the whole
+// tile, the int32 group accumulators only for two fragment rows at a time (row-pipelined fold,
+// below), which is what lets the 128 x 64 wave tile fit without spills. One 128-B K stage = 256 int4 = two groups: MFMA steps 0-1 form group 2s, steps
 // 2-3 group 2s+1, each group's first MFMA starting from a zero accumulator operand. The widened
 // nibbles make acc = 256 * sum(a*b) (exact, |acc| < 2^22); the fold runs on that raw value and the
 // store multiplies by 2^-8 — power-of-two scaling commutes with every rounding here (all partial
