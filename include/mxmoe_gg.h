@@ -97,7 +97,7 @@ const char* mxmoe_gg_last_error(void);
 /* Number of compiled kernel variants. */
 int mxmoe_gg_variant_count(void);
 
-/* The variant AUTO resolves to unless every non-empty problem is w4a4. */
+/* The variant AUTO resolves to for long-K calls that are not w4a4-only (mxmoe_gg_resolve_variant). */
 int mxmoe_gg_default_variant(void);
 
 /* Writes a newline-separated description of every compiled variant into buf (truncated,
@@ -114,6 +114,12 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
 /* Pass as `variant` to mxmoe_gg_workspace_size / _plan / _run: the library picks the variant
  * from the quant types present (the plan info records the concrete one). groupgemm_mxmoe uses it. */
 #define MXMOE_GG_VARIANT_AUTO (-1)
+
+/* The concrete variant `variant` (MXMOE_GG_VARIANT_AUTO or an index) resolves to for these
+ * problems, written to *out. Host only (no GPU). AUTO: w4a4-only sets -> the 256x128 2-WG/CU
+ * kernel (unless the plan needs split-K); calls whose median tile has <= 24 128-B K stages ->
+ * the 3-stage-B-ring staggered kernel; otherwise mxmoe_gg_default_variant(). */
+int mxmoe_gg_resolve_variant(const mxmoe_gg_problem* problems, int problem_count, int variant, int* out);
 
 /* Device workspace bytes the plan of these problems needs with this variant
  * (plan table + pointer arrays + tile table). Validates the problems like mxmoe_gg_plan. */

@@ -73,7 +73,7 @@ class GGPlanInfo(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
-    "mxmoe_gg_variant_tile", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
+    "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
     "groupgemm_mxmoe", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     # include/mxmoe_moe.h (MoE-layer plumbing)
     "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_combine",
@@ -103,6 +103,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_list_variants.argtypes = [c.c_char_p, c.c_size_t]
     lib.mxmoe_gg_variant_tile.restype = c.c_int
     lib.mxmoe_gg_variant_tile.argtypes = [c.c_int, c.c_int, c.c_int] + [c.POINTER(c.c_int32)] * 4
+    lib.mxmoe_gg_resolve_variant.restype = c.c_int
+    lib.mxmoe_gg_resolve_variant.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.POINTER(c.c_int)]
     lib.mxmoe_gg_workspace_size.restype = c.c_int
     lib.mxmoe_gg_workspace_size.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.POINTER(c.c_size_t)]
     lib.mxmoe_gg_plan.restype = c.c_int
@@ -189,6 +191,13 @@ def repack_weightonly(ref_words, N: int, K: int, w_bits: int):
     out = np.empty((N, K * w_bits // 8), dtype=np.uint8)
     check(lib().mxmoe_gg_repack_weightonly(src.ctypes.data, N, K, w_bits, out.ctypes.data))
     return out
+
+
+def resolve_variant(problems, problem_count: int, variant: int = VARIANT_AUTO) -> int:
+    """The concrete variant AUTO (or an index) resolves to for a ctypes array of GGProblemC (host only)."""
+    out = ctypes.c_int()
+    check(lib().mxmoe_gg_resolve_variant(problems, problem_count, variant, ctypes.byref(out)))
+    return out.value
 
 
 def workspace_size(problems, problem_count: int, variant: int) -> int:

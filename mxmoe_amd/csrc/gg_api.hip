@@ -74,7 +74,7 @@ void launch_v2_q(const GGArgs& a, int grid, hipStream_t s) {
 }
 template <int ABL>
 void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
-  if constexpr ((ABL & 7) != 0) {
+  if constexpr ((ABL & kAblMask) != 0) {
     launch_v2_q<ABL, 7>(a, grid, s);
   } else {
     switch (qmask & 63) {
@@ -154,7 +154,7 @@ Variant make_v2(const char* name) {
   v.geom[QT_W8A16] = {256, 256, 64, 512};
   v.geom[QT_I4G] = {256, 256, 128, 512};  // w4a4 g128 (gg_tile_g128): 256 / 128-row classes as int4
   v.threads = 512;
-  v.lds_bytes = V2Cfg<256>::LDS_BYTES;
+  v.lds_bytes = (ABL & V2_B3) ? 160 * 1024 : V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
   v.k_stage_bytes = 0;  // K tails handled in-kernel (last stage)
   v.tail_bm = 128;
@@ -186,6 +186,12 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | ABL_NO_DMA | ABL_NO_EPI>("abl_v2s_nodma_noepi"),
       make_v2<V2_STAGGER | V2_TRACE>("abl_v2s_trace"),
       make_v2<V2_STAGGER | ABL_DMA_HOT>("abl_v2s_dmahot"),
+      // where the DMA cost goes (v2, WRONG RESULTS by design; int8 tiles only)
+      make_v2<ABL_B_NODMA>("abl_v2_b_nodma"),
+      make_v2<ABL_B_REGLOAD>("abl_v2_b_regload"),
+      make_v2<ABL_B_TILED>("abl_v2_b_tiled"),
+      // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB): AUTO for short-K calls
+      make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
   };
   return v;
 }
@@ -195,6 +201,11 @@ const std::vector<Variant>& variants() {
 // unless they are low-fill enough to need split-K (v2 kernels only).
 constexpr const char* kDefaultVariantName = "v2s_256x256_w8_dma_stagger";
 constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
+// short-K calls (median tile <= kShortKStages 128-B K stages, e.g. the qwen2_moe down GroupGEMM:
+// K = 1408): B two stages ahead pays for its 160-KiB LDS image (profiles/r01/session3, +3-5 % on
+// fp16 / w8a8 down, routed problems +7-9 %; +-1 % on gate_up, -1..3 % on dense 8192^3)
+constexpr const char* kShortKVariant = "v2s3_256x256_w8_dma_stagger_bring3";
+constexpr int kShortKStages = 24;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
@@ -497,6 +508,26 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     // to split K (that kernel cannot)
     Plan p;
     if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == 0) *out = variant_index(kInt4Variant);
+  } else if (mask & ((1 << QT_F16) | (1 << QT_I8) | (1 << QT_I4))) {
+    std::vector<std::pair<int, int64_t>> st;  // (128-B K stages, tiles) of the fp16 / w8a8 / w4a4 problems
+    int64_t total = 0;
+    for (const HostProblem& p : hp) {
+      int qt;
+      if (p.M <= 0 || qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) != MXMOE_GG_OK) continue;
+      if (qt != QT_F16 && qt != QT_I8 && qt != QT_I4) continue;
+      const int64_t tiles = (int64_t)((p.M + 255) / 256) * ((p.N + 255) / 256);
+      st.emplace_back((int)(((int64_t)p.K * p.a_bits / 8 + 127) / 128), tiles);
+      total += tiles;
+    }
+    std::sort(st.begin(), st.end());
+    int64_t acc = 0;
+    for (const auto& e : st) {
+      acc += e.second;
+      if (2 * acc >= total) {
+        if (e.first <= kShortKStages) *out = variant_index(kShortKVariant);
+        break;
+      }
+    }
   }
   return MXMOE_GG_OK;
 }
@@ -603,6 +634,13 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
   if (bk_bytes) *bk_bytes = g.bkb;
   if (threads) *threads = g.threads;
   return MXMOE_GG_OK;
+}
+
+int mxmoe_gg_resolve_variant(const mxmoe_gg_problem* problems, int problem_count, int variant, int* out) {
+  if (!out) return fail(MXMOE_GG_ERR_INVALID, "out is NULL");
+  if (problem_count < 0 || (problem_count > 0 && !problems))
+    return fail(MXMOE_GG_ERR_INVALID, "bad problem array (count %d)", problem_count);
+  return resolve_variant(variant, to_host(problems, problem_count), out);
 }
 
 int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count, int variant, size_t* bytes) {

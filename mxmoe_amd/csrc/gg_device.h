@@ -498,10 +498,17 @@ __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& 
 
 // ABL flags. Timing ablations (results are garbage): 1 = no mainloop DMA (stage 0 reused),
 // 2 = no LDS fragment reads (register fragments), 4 = no epilogue stores, 16 = every stage's
-// LDS-DMA re-reads the tile's first K slice (same LDS traffic, L2-hot sources).
-// Options (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3;
-// 64 = tile timeline trace (diagnostics).
-enum : int { ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8, ABL_DMA_HOT = 16, V2_TRACE = 64 };
+// LDS-DMA re-reads the tile's first K slice (same LDS traffic, L2-hot sources), 512 / 1024 / 2048
+// (below). Options (correct results): 8 = stagger — waves 4-7 run half a stage behind waves 0-3;
+// 4096 = B ring of three stages (with the stagger); 64 = tile timeline trace (diagnostics).
+enum : int {
+  ABL_NO_DMA = 1, ABL_NO_LDS = 2, ABL_NO_EPI = 4, V2_STAGGER = 8, ABL_DMA_HOT = 16, V2_TRACE = 64,
+  ABL_B_NODMA = 512,    // ablation: B operand never loaded (A only)
+  ABL_B_REGLOAD = 1024,  // ablation: B operand loaded into registers (same global traffic), not into LDS
+  ABL_B_TILED = 2048,    // ablation: B read as if stored in contiguous 32-KiB (256 rows x 128 B) stage blocks
+  V2_B3 = 4096           // stagger: B in a 3-stage LDS ring, two stages ahead (A: 2 stages, one ahead)
+};
+constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
 
 // Tile timeline (diagnostics, V2_TRACE builds only): per block {start, mainloop end, end (stores
 // drained), nst << 48 | class << 40 | qtype << 36 | XCC_ID << 32 | HW_ID}, s_memrealtime ticks
@@ -515,6 +522,25 @@ __device__ __forceinline__ void trace_mark(int slot) {
 // One 64-B K half of a v2 stage (128-B rows, XOR-swizzled 16-B chunks) as raw fragment words:
 // read from LDS, then consumed by the MFMAs (int4 widened at use). Used by the staggered v2
 // mainloop (gg_tile_v2 with V2_STAGGER).
+// One operand's 128-B K stage of G x 8 rows per wave into a lane-linear LDS image (v2 layout); the
+// K tail (last stage only) loads 16 zero bytes for chunks past K.
+template <int G>
+__device__ __forceinline__ void v2_dma(const uint8_t* const (&src)[G], uint8_t* dst, int kb, int kbytes, int wave,
+                                       int lane) {
+  if (kb + 128 <= kbytes) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) glds16(src[j] + kb, dst + (wave * G + j) * 1024);
+  } else {
+    const int rsub = lane >> 3, p = lane & 7;
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(g_zero16);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int kc = (p ^ ((((wave * G + j) * 8 + rsub) >> 1) & 7)) << 4;
+      glds16(kb + kc < kbytes ? src[j] + kb : zero, dst + (wave * G + j) * 1024);
+    }
+  }
+}
+
 template <class Cfg, int QT>
 struct V2Half {
   typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
@@ -523,9 +549,10 @@ struct V2Half {
   word_t a[SUBH][FM];
   word_t b[SUBH][FN];
 
-  __device__ __forceinline__ void read(const uint8_t* stage, uint32_t a_row, uint32_t b_row, int swz, int g, int h) {
-    const uint8_t* As = stage + a_row;
-    const uint8_t* Bs = stage + Cfg::A_BYTES + b_row;
+  __device__ __forceinline__ void read(const uint8_t* abase, const uint8_t* bbase, uint32_t a_row, uint32_t b_row, int swz,
+                                       int g, int h) {
+    const uint8_t* As = abase + a_row;
+    const uint8_t* Bs = bbase + b_row;
 #pragma unroll
     for (int t = 0; t < SUBH; ++t) {
       const uint32_t off = QT == QT_I4 ? (uint32_t)(((2 * (2 * h + t) + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8)
@@ -598,8 +625,11 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       const int row = (wave * GB + j) * 8 + rsub;
       const int grow = min(n0 + row, N - 1);
       srcB[j] = B + (int64_t)grow * ldb + ((p ^ ((row >> 1) & 7)) << 4);
+      if constexpr ((ABL & ABL_B_TILED) != 0)  // block (n0/256, stage) at ((n0/256)*nstages + stage)*32 KiB
+        srcB[j] = B + (int64_t)(n0 / 256) * ((kbytes + 127) / 128) * 32768 + row * 128 + ((p ^ ((row >> 1) & 7)) << 4);
     }
   }
+  uint4 breg[GB];  // ABL_B_REGLOAD sink
   auto issue = [&](int s, int buf) {
     if constexpr ((ABL & ABL_NO_DMA) != 0) {
       if (s > 0) return;
@@ -610,8 +640,16 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     if (kb + Cfg::BKB <= kbytes) {
 #pragma unroll
       for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
+      if constexpr ((ABL & ABL_B_REGLOAD) != 0) {
 #pragma unroll
-      for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
+        for (int j = 0; j < GB; ++j) breg[j] = *reinterpret_cast<const uint4*>(srcB[j] + kb);
+      } else if constexpr ((ABL & ABL_B_TILED) != 0) {
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16(srcB[j] + (int64_t)kb * 256, Bs + (wave * GB + j) * 1024);
+      } else if constexpr ((ABL & ABL_B_NODMA) == 0) {
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
+      }
     } else {
       // K tail (last stage only): chunks past K load 16 zero bytes instead
       const int rsub = lane >> 3, p = lane & 7;
@@ -718,9 +756,59 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   // Waves 4-7 instead defer the second K half of every stage past the barrier, holding its
   // fragments in registers: after each barrier they start on MFMAs while waves 0-3 start on LDS
   // reads. Every accumulator still sees its K chunks in order -> bit-identical results.
-  if constexpr ((ABL & V2_STAGGER) != 0) {
+  if constexpr ((ABL & V2_STAGGER) != 0 && (ABL & V2_B3) != 0) {
+    // B3: A ring of 2 stages at [0, 2 A_BYTES), B ring of 3 at [2 A_BYTES, + 3 B_BYTES). Stage s+1's
+    // A and stage s+2's B are issued at the top of stage s; the barrier at its end waits for
+    // everything but B(s+2) (issued last: vmcnt(GB)). A(s+1) refills the A buffer and B(s+2) the B
+    // buffer stage s-1 was read from (every wave's reads of it completed before the last barrier).
     typedef V2Half<Cfg, QT> Half;
-    auto hread = [&](Half& f, int buf, int h) { f.read(lds + buf * Cfg::STAGE_BYTES, a_row, b_row, swz, g, h); };
+    auto abuf = [&](int s) { return lds + (s & 1) * Cfg::A_BYTES; };
+    auto bbuf = [&](int s) { return lds + 2 * Cfg::A_BYTES + (s % 3) * Cfg::B_BYTES; };
+    auto issue_a = [&](int s) { v2_dma<GA>(srcA, abuf(s), (ks0 + s) * Cfg::BKB, kbytes, wave, lane); };
+    auto issue_b = [&](int s) { v2_dma<GB>(srcB, bbuf(s), (ks0 + s) * Cfg::BKB, kbytes, wave, lane); };
+    auto hread = [&](Half& f, int s, int h) { f.read(abuf(s), bbuf(s), a_row, b_row, swz, g, h); };
+    auto hmma = [&](const Half& f) { f.mma(acc); };
+    auto sync_next = [&](int s) {  // stage s+1 landed for every wave
+      if (s + 2 < nst) wait_vmcnt<GB>();
+      else wait_vmcnt<0>();
+      lds_barrier();
+    };
+    if (nst > 0) {
+      Half fr;
+      issue_a(0);
+      issue_b(0);
+      if (nst > 1) issue_b(1);
+      sync_next(-1);
+      if (wave >= Cfg::WM * Cfg::WN / 2) {
+        for (int s = 0; s < nst; ++s) {
+          if (s + 1 < nst) issue_a(s + 1);
+          if (s + 2 < nst) issue_b(s + 2);
+          if (s > 0) hmma(fr);
+          hread(fr, s, 0);
+          hmma(fr);
+          hread(fr, s, 1);
+          sync_next(s);
+        }
+        hmma(fr);
+      } else {
+        for (int s = 0; s < nst; ++s) {
+          if (s + 1 < nst) issue_a(s + 1);
+          if (s + 2 < nst) issue_b(s + 2);
+          hread(fr, s, 0);
+          hmma(fr);
+          hread(fr, s, 1);
+          hmma(fr);
+          sync_next(s);
+        }
+      }
+    }
+    stash_scale();  // the rings are dead: the scale stash (past the epilogue image) is free
+    if constexpr (QT != QT_F16) __syncthreads();
+  } else if constexpr ((ABL & V2_STAGGER) != 0) {
+    typedef V2Half<Cfg, QT> Half;
+    auto hread = [&](Half& f, int buf, int h) {
+      f.read(lds + buf * Cfg::STAGE_BYTES, lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES, a_row, b_row, swz, g, h);
+    };
     auto hmma = [&](const Half& f) { f.mma(acc); };
     auto stage_sync = [&](int) { __syncthreads(); };  // stage s+1 landed, buffer s&1 released
     if (nst > 0) {
@@ -757,11 +845,15 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     for (int s = 0; s < nst; ++s) {
       if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
       compute(s & 1);
+      if constexpr ((ABL & ABL_B_REGLOAD) != 0) {
+#pragma unroll
+        for (int j = 0; j < GB; ++j) asm volatile("" ::"v"(breg[j].x), "v"(breg[j].y), "v"(breg[j].z), "v"(breg[j].w));
+      }
       __syncthreads();  // own LDS-DMA landed (vmcnt(0)); every wave done reading buffer s&1
     }
   }
 
-  if (nst <= 0) {  // no mainloop barrier behind the stash
+  if ((ABL & V2_B3) == 0 && nst <= 0) {  // no mainloop barrier behind the stash
     stash_scale();
     __syncthreads();
   }
@@ -769,6 +861,11 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
 
   // ---- epilogue: per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----
+  // (B3: the lane decomposition is recomputed from an opaque copy of the thread id, so the
+  // compiler does not keep it live — and spilled — across the 160-KiB mainloop)
+  int etid = tid;
+  if constexpr ((ABL & V2_B3) != 0) asm volatile("" : "+v"(etid));
+  const int e_lane = etid & 63, e_r16 = e_lane & 15, e_g = e_lane >> 4;
   uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
   const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
   // int paths: the tile's row / column scales were staged in LDS during the prologue
@@ -776,11 +873,11 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   uint2 sbw[FN];
   if constexpr (QT != QT_F16) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * g);
+    for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * e_g);
   }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int ml = i * 16 + r16;
+    const int ml = i * 16 + e_r16;
     _Float16 sai = 0;
     if constexpr (QT != QT_F16) sai = sl[wm * Cfg::WTM + ml];
 #pragma unroll
@@ -788,14 +885,14 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       uint2 pk;
       if constexpr (QT == QT_F16) pk = pack4_f16(acc[i][j]);
       else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
-      const int q = 2 * j + (g >> 1);
-      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (g & 1) * 8) = pk;
+      const int q = 2 * j + (e_g >> 1);
+      *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
     }
   }
   // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
 #pragma unroll 4
   for (int it = 0; it < Cfg::WTM / 8; ++it) {
-    const int row = it * 8 + (lane >> 3), q = lane & 7;
+    const int row = it * 8 + (e_lane >> 3), q = e_lane & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
     const int m = mrow0 + row, n = ncol0 + q * 8;
     if constexpr ((ABL & ABL_NO_EPI) != 0) {
@@ -1057,7 +1154,7 @@ struct V3Cfg {
   static constexpr int LDS_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
   static_assert(WTN == 64 || WTN == 128, "epilogue stages 128-B or 256-B rows");
   static_assert(GA >= 1 && GB >= 1, "each wave issues at least one DMA per operand");
-  static_assert(DIST < NBUF && DIST <= 3, "ring: stage s+DIST reuses the buffer of stage s-1 at most");
+  static_assert(DIST < NBUF && DIST <= 4, "ring: stage s+DIST reuses the buffer of stage s-1 at most");
 };
 
 __device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }  // T = {0,2,3,1}
@@ -1221,7 +1318,8 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
     if (p < nst) issue(p);
   for (int s = 0; s < nst; ++s) {
     const int later = min(Cfg::DIST - 1, nst - 1 - s);  // stages issued after s so far
-    if (later >= 2) wait_vmcnt<2 * DPS>();
+    if (later >= 3) wait_vmcnt<(Cfg::DIST >= 4 ? 3 : 2) * DPS>();
+    else if (later == 2) wait_vmcnt<2 * DPS>();
     else if (later == 1) wait_vmcnt<DPS>();
     else wait_vmcnt<0>();
     lds_barrier();  // stage s landed for every wave; every wave is done with buffer (s-1)%4
@@ -1494,7 +1592,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
 __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   // + the int paths' scale stash: SA at [LDS_BYTES, +2*BM), SB at [LDS_BYTES + 512, +512)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[(ABL & V2_B3) ? 160 * 1024 : V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA];
   if constexpr ((ABL & V2_TRACE) != 0) trace_mark(0);
   const TileDesc td = args.tiles[blockIdx.x];
   if (td.prob < 0) return;
@@ -1519,7 +1617,7 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v2<V2Cfg<128>, QT_I8, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);  // no 64-row class
-  } else if constexpr ((ABL & 7) != 0) {
+  } else if constexpr ((ABL & kAblMask) != 0) {
     return;  // ablation builds time the int8 path only
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_I4, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);

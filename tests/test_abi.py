@@ -85,6 +85,32 @@ def test_auto_variant_follows_quant_mix():
     assert ws(w4 + [_prob(M=0)], nat.VARIANT_AUTO) == ws(w4 + [_prob(M=0)], int4_v)
 
 
+def test_auto_variant_short_k_rule():
+    """AUTO: median tile <= 24 128-B K stages -> the 3-stage-B-ring kernel; longer K -> the default."""
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    b3 = names.index("v2s3_256x256_w8_dma_stagger_bring3")
+
+    def auto(ps):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.resolve_variant(arr, len(ps))
+
+    f16 = dict(a_bits=16, w_bits=16, scale_a=0, scale_b=0)
+    assert auto([_prob(M=4096, N=4096, K=2048, **f16)]) == nat.default_variant()  # 32 stages
+    assert auto([_prob(M=4096, N=4096, K=1408, **f16)]) == b3  # 22 stages
+    assert auto([_prob(M=4096, N=4096, K=2048)]) == b3  # int8: 16 stages
+    assert auto([_prob(M=4096, N=4096, K=4096)]) == nat.default_variant()  # int8: 32 stages
+    # the median is tile-weighted: one big long-K problem outweighs several small short-K ones
+    assert auto([_prob(M=8192, N=8192, K=4096, **f16)] + [_prob(M=256, N=256, K=256, **f16)] * 4) == \
+        nat.default_variant()
+    from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
+
+    layer = load_workload(qwen2_layer11_workload(8192))["layer-11"]
+    for gg, want in (("gate_up", nat.default_variant()), ("down", b3)):
+        probs = [_prob(M=s.M, N=s.N, K=s.K, **f16) for s in layer[gg]]
+        assert auto(probs) == want, gg
+    assert auto([_prob(M=64, N=128, K=256)]) == nat.resolve_variant((nat.GGProblemC * 1)(_prob(M=64, N=128, K=256)), 1, b3)
+
+
 def _plan(problems, ws_bytes=1 << 20):
     arr = (nat.GGProblemC * len(problems))(*problems)
     info = nat.GGPlanInfo()
