@@ -161,8 +161,19 @@ __device__ __forceinline__ _Float16 rtn_scale(float amax, float qmax) {
   _Float16 s = (_Float16)(amax / qmax);
   return s == (_Float16)0 ? (_Float16)1 : s;
 }
-__device__ __forceinline__ int rtn_code(_Float16 x, _Float16 s, float qmax) {
-  float d = (float)(_Float16)((float)x / (float)s);
+// fp16(f32(x) / f32(s)) without the IEEE divide sequence (~10 VALU, which made these kernels
+// VALU-bound): q = x * r, one Newton step q' = q + (x - q s) r with r = v_rcp_f32(s) (<= 1 ulp).
+// q' is within 0.5 ulp (+ 2^-46 relative) of x / s. For fp16 x and s (11-bit significands) x / s is
+// at least 1 / ((2^11 - 1)(2^12 - 1)) > 2^-23 (relative) away from every fp16 rounding midpoint
+// (a 12-bit odd significand M with |x - M s| > 0 is at least one unit of the 23-bit product M s),
+// so q' and the correctly rounded quotient lie on the same side of every midpoint and round to the
+// same fp16 — bit-exact with the IEEE division the oracle uses.
+__device__ __forceinline__ float div_f16_operands(float x, float s, float r) {
+  const float q = x * r;
+  return fmaf(fmaf(-q, s, x), r, q);
+}
+__device__ __forceinline__ int rtn_code(_Float16 x, _Float16 s, float rs, float qmax) {
+  float d = (float)(_Float16)div_f16_operands((float)x, (float)s, rs);
   d = fminf(fmaxf(d, -qmax), qmax);
   return (int)__builtin_rintf(d);
 }
@@ -243,9 +254,10 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
       for (int d = 8; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
       if (idx < width) {
         const _Float16 sc = rtn_scale(m, qmax);
+        const float rs = __builtin_amdgcn_rcpf((float)sc);
         int q[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, qmax);
+        for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, rs, qmax);
         *reinterpret_cast<uint32_t*>(o + idx / 2) = pack_i4x8(q);
         if ((lane & 15) == 0) a.scales[sg.scale_off + (int64_t)(idx / 128) * sg.rows + row] = sc;
       }
@@ -260,6 +272,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
   const _Float16 sc = rtn_scale(m, qmax);
+  const float rs = __builtin_amdgcn_rcpf((float)sc);
   if (lane == 0) a.scales[sg.scale_off + row] = sc;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
@@ -267,7 +280,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
     if (idx >= width) continue;
     int q[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, qmax);
+    for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, rs, qmax);
     if (bits == 8) {
       *reinterpret_cast<uint2*>(o + idx) = uint2{pack_i8x4(q[0], q[1], q[2], q[3]), pack_i8x4(q[4], q[5], q[6], q[7])};
     } else {

@@ -232,3 +232,30 @@ def test_moe_ffn_stagewise_parity(gpu):
     ref = moe_ref.combine(y.cpu().numpy(), r.inv_slot.cpu().numpy(), wts.numpy(), topk, ys.cpu().numpy())
     assert (out.cpu().numpy().view(np.uint16) == ref.view(np.uint16)).all()
     assert torch.isfinite(out.float()).all()
+
+
+def test_fast_quotient_matches_ieee_division():
+    """moe_ops.hip div_f16_operands: q = x*r, q' = fma(fma(-q, s, x), r, q) with r = rcp(s) within
+    1 ulp rounds to the same fp16 as the IEEE f32 quotient for fp16 x and s (the quantiser's
+    fp16(x / scale)). Checked here for every positive finite fp16 scale, 64 random x per scale in
+    the quantiser's range |x / s| <= 130, and r correctly rounded or 1 ulp off either way; fma is
+    emulated exactly in float64 (24-bit x 24-bit products are exact there). Signed zeros may
+    differ (-0 vs +0); the integer codes cannot."""
+    import warnings
+
+    rng = np.random.default_rng(0)
+    s_all = np.arange(1, 0x7C00, dtype=np.uint16).view(np.float16).astype(np.float32)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for _ in range(64):
+            x = (rng.uniform(-130, 130, size=s_all.shape).astype(np.float32) * s_all).astype(np.float16)
+            ok = np.isfinite(x)
+            x, s = x[ok].astype(np.float32), s_all[ok]
+            ref = np.rint(np.clip((x / s).astype(np.float16).astype(np.float32), -127, 127))
+            r0 = (np.float32(1) / s).astype(np.float32)
+            for r in (r0, np.nextafter(r0, np.float32(np.inf)), np.nextafter(r0, np.float32(0))):
+                q = (x * r).astype(np.float32)
+                e = (x.astype(np.float64) - q.astype(np.float64) * s).astype(np.float32)
+                q2 = (e.astype(np.float64) * r + q.astype(np.float64)).astype(np.float32)
+                got = np.rint(np.clip(q2.astype(np.float16).astype(np.float32), -127, 127))
+                assert (got == ref).all()
