@@ -142,19 +142,6 @@ struct ActArgs {
   _Float16* scales;
 };
 
-__device__ __forceinline__ uint32_t pack_i8x4(int q0, int q1, int q2, int q3) {
-  // pack_wxax int8: word j = (q[2j] << 8) | q[2j+1] little-endian -> bytes q[2j+1], q[2j]
-  return (uint32_t)(q1 & 0xFF) | ((uint32_t)(q0 & 0xFF) << 8) | ((uint32_t)(q3 & 0xFF) << 16) |
-         ((uint32_t)(q2 & 0xFF) << 24);
-}
-__device__ __forceinline__ uint32_t pack_i4x8(const int (&q)[8]) {
-  // pack_wxax int4: word j = q[4j]<<12 | q[4j+1]<<8 | q[4j+2]<<4 | q[4j+3]
-  //   -> byte 2j = (q[4j+2] << 4) | q[4j+3], byte 2j+1 = (q[4j] << 4) | q[4j+1]
-  const uint32_t b0 = ((q[2] & 0xF) << 4) | (q[3] & 0xF), b1 = ((q[0] & 0xF) << 4) | (q[1] & 0xF);
-  const uint32_t b2 = ((q[6] & 0xF) << 4) | (q[7] & 0xF), b3 = ((q[4] & 0xF) << 4) | (q[5] & 0xF);
-  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
-}
-
 // quant_weight arithmetic (quantize.cuh:218-279): scale = fp16(amax / qmax), 0 -> 1;
 // q = rint_even(clamp(fp16(x / scale), -qmax, qmax))
 __device__ __forceinline__ _Float16 rtn_scale(float amax, float qmax) {
@@ -172,10 +159,45 @@ __device__ __forceinline__ float div_f16_operands(float x, float s, float r) {
   const float q = x * r;
   return fmaf(fmaf(-q, s, x), r, q);
 }
-__device__ __forceinline__ int rtn_code(_Float16 x, _Float16 s, float rs, float qmax) {
-  float d = (float)(_Float16)div_f16_operands((float)x, (float)s, rs);
-  d = fminf(fmaxf(d, -qmax), qmax);
-  return (int)__builtin_rintf(d);
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+
+// Codes of elements 2p, 2p+1 of x: d = fp16(x / s) clamped to +-qmax in fp16 (exact), then
+// d + 1536 in fp16: for |d| <= 127 the sum lies in [1024, 2048) where the fp16 spacing is 1, so
+// the add rounds d to an integer with ties to even (1536 is even: rint's tie rule), and the low
+// byte of the sum's bits (mantissa 512 + rint(d)) is rint(d)'s two's-complement byte. Returns the
+// pair's bits: code(2p) in byte 0, code(2p+1) in byte 2.
+__device__ __forceinline__ uint32_t pair_codes(const h8_t& x, int p, float s, float r, h2_t lim) {
+  h2_t d = {(_Float16)div_f16_operands((float)x[2 * p], s, r), (_Float16)div_f16_operands((float)x[2 * p + 1], s, r)};
+  d = __builtin_elementwise_min(__builtin_elementwise_max(d, -lim), lim);
+  d = d + h2_t{(_Float16)1536, (_Float16)1536};
+  return __builtin_bit_cast(uint32_t, d);
+}
+// pack_wxax (quantize.cuh:425-475) stores element j+x of a 16-bit word at bits (PACK-1-x)*bits:
+// int8 word j = q[2j] << 8 | q[2j+1] (little-endian bytes q[2j+1], q[2j]); int4 word j =
+// q[4j] << 12 | q[4j+1] << 8 | q[4j+2] << 4 | q[4j+3].
+// order4: 4 codes from two pair words as bytes [q1, q0, q3, q2] (v_perm_b32: selectors 0-3 take
+// the second operand's bytes, 4-7 the first's)
+__device__ __forceinline__ uint32_t order4(uint32_t p01, uint32_t p23) { return __builtin_amdgcn_perm(p23, p01, 0x04060002u); }
+// int8: 8 codes -> 8 packed bytes
+__device__ __forceinline__ uint2 codes_i8(const h8_t& x, float s, float r, h2_t lim) {
+  return uint2{order4(pair_codes(x, 0, s, r, lim), pair_codes(x, 1, s, r, lim)),
+               order4(pair_codes(x, 2, s, r, lim), pair_codes(x, 3, s, r, lim))};
+}
+// int4: from [q1, q0, q3, q2] nibbles, t = a | a >> 4 puts (q0 << 4 | q1) in byte 0 and
+// (q2 << 4 | q3) in byte 2; the word is bytes [t.2, t.0, u.2, u.0] (pack_i4x8 order)
+__device__ __forceinline__ uint32_t codes_i4(const h8_t& x, float s, float r, h2_t lim) {
+  const uint32_t a = order4(pair_codes(x, 0, s, r, lim), pair_codes(x, 1, s, r, lim)) & 0x0F0F0F0Fu;
+  const uint32_t b = order4(pair_codes(x, 2, s, r, lim), pair_codes(x, 3, s, r, lim)) & 0x0F0F0F0Fu;
+  return __builtin_amdgcn_perm(b | (b >> 4), a | (a >> 4), 0x04060002u);
+}
+// max |x| over 8 fp16 (exact in fp16: v_pk_max_f16 on sign-cleared pairs)
+__device__ __forceinline__ float amax8(const h8_t& x) {
+  const uint4 w = __builtin_bit_cast(uint4, x);
+  const uint32_t m = 0x7FFF7FFFu;
+  const h2_t a = __builtin_elementwise_max(__builtin_bit_cast(h2_t, w.x & m), __builtin_bit_cast(h2_t, w.y & m));
+  const h2_t b = __builtin_elementwise_max(__builtin_bit_cast(h2_t, w.z & m), __builtin_bit_cast(h2_t, w.w & m));
+  const h2_t c = __builtin_elementwise_max(a, b);
+  return fmaxf((float)c[0], (float)c[1]);
 }
 
 // One WAVE per slot row (4 rows per 256-thread workgroup): lane l holds elements c*512 + 8l .. +7
@@ -241,24 +263,20 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   }
   const int bits = sg.qtag == MXMOE_ACT_INT8 ? 8 : 4;
   const float qmax = bits == 8 ? 127.0f : 7.0f;
+  const h2_t lim = {(_Float16)qmax, (_Float16)qmax};
   uint8_t* o = a.out + sg.out_off + row * (int64_t)width * bits / 8;
   if (sg.qtag == MXMOE_ACT_INT4_G128) {
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       if (c * 512 >= width) break;  // uniform
       const int idx = c * 512 + lane * 8;
-      float m = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)x[c][j]));
+      float m = amax8(x[c]);
 #pragma unroll
       for (int d = 8; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
       if (idx < width) {
         const _Float16 sc = rtn_scale(m, qmax);
         const float rs = __builtin_amdgcn_rcpf((float)sc);
-        int q[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, rs, qmax);
-        *reinterpret_cast<uint32_t*>(o + idx / 2) = pack_i4x8(q);
+        *reinterpret_cast<uint32_t*>(o + idx / 2) = codes_i4(x[c], (float)sc, rs, lim);
         if ((lane & 15) == 0) a.scales[sg.scale_off + (int64_t)(idx / 128) * sg.rows + row] = sc;
       }
     }
@@ -266,9 +284,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   }
   float m = 0.0f;
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)x[c][j]));
+  for (int c = 0; c < MAXC; ++c) m = fmaxf(m, amax8(x[c]));  // chunks past the row are zeros
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
   const _Float16 sc = rtn_scale(m, qmax);
@@ -278,14 +294,8 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   for (int c = 0; c < MAXC; ++c) {
     const int idx = c * 512 + lane * 8;
     if (idx >= width) continue;
-    int q[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) q[j] = rtn_code(x[c][j], sc, rs, qmax);
-    if (bits == 8) {
-      *reinterpret_cast<uint2*>(o + idx) = uint2{pack_i8x4(q[0], q[1], q[2], q[3]), pack_i8x4(q[4], q[5], q[6], q[7])};
-    } else {
-      *reinterpret_cast<uint32_t*>(o + idx / 2) = pack_i4x8(q);
-    }
+    if (bits == 8) *reinterpret_cast<uint2*>(o + idx) = codes_i8(x[c], (float)sc, rs, lim);
+    else *reinterpret_cast<uint32_t*>(o + idx / 2) = codes_i4(x[c], (float)sc, rs, lim);
   }
 }
 
