@@ -14,8 +14,10 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -368,9 +370,10 @@ struct Plan {
 //     then one tail_bm (128) or tail2_bm (64) tile), n-tiles of width bn; 4-m-tile bands, n-major
 //     inside a band, so 32 consecutive tiles form a ~4 x 8 block sharing A rows and B columns;
 //  2. problems by descending per-tile cost (K bytes x tile area x MFMA passes), longest first;
-//  3. the sequence is cut into chunks of `chunk` tiles; chunk c runs on XCD c % 8 in round c / 8:
-//     blockIdx = 8 * (chunk * round + position) + c % 8 (blocks b and b + 8 share an XCD under the
-//     round-robin dispatch; placement affects speed only, never results).
+//  3. the sequence is cut into chunks of `chunk` tiles; each chunk in turn joins the queue of the
+//     XCD with the least modelled time so far (tile_time); XCD x's i-th tile is blockIdx 8 i + x
+//     (blocks b and b + 8 share an XCD under the round-robin dispatch; placement affects speed
+//     only, never results).
 int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptrs, Plan* plan) {
   const Variant& v = variants()[variant];
   const int P = (int)probs.size();
@@ -438,7 +441,27 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       if (ratio > 2.0 && all[i].qtype != QT_I4G) split[i] = std::max(1, std::min({8, (int)ratio, stages_of(all[i]) / 4}));
     }
   }
-  auto tile_cost = [&](int i) { return full_tile_cost(i) / split[i]; };
+  // Tile time model (per K stage, in "bytes": one stage's LDS-DMA bytes or its MFMA work at the
+  // fp16 rate of 128 flop/B, whichever is larger, plus a fixed 24 KiB-equivalent per stage).
+  // Fitted to the tile timelines (profiles/r01/session3/trace_bs512.jsonl): 64-row /
+  // 256-row tile time ratios 1.3 (fp16) and 2.1 (w4a16), where tile area alone says 4.
+  auto stage_time = [&](const GGMeta& m, int cls) {
+    const TileGeom& g = v.geom[m.qtype];
+    const double rows = class_rows(cls, g), cols = g.bn;
+    double bytes, equiv;
+    if (m.qtype == QT_W4A16 || m.qtype == QT_W8A16) {  // 64 K elements per stage, fp16 A
+      bytes = rows * 128 + cols * 64 * (m.qtype == QT_W4A16 ? 4 : 8) / 8.0;
+      equiv = 2.0 * rows * cols * 64 / 128;
+    } else {
+      const double kel = g.bkb * 8.0 / (m.qtype == QT_F16 ? 16 : m.qtype == QT_I8 ? 8 : 4);
+      const double rate = m.qtype == QT_F16 ? 128 : 256, fold = m.qtype == QT_I4G ? 1.25 : 1.0;
+      bytes = (rows + cols) * g.bkb;
+      equiv = 2.0 * rows * cols * kel / rate * fold;
+    }
+    return std::max(bytes, equiv) + 24576.0;
+  };
+  // problems by the modelled time of their first (tallest) tile, longest first
+  auto tile_cost = [&](int i) { return stage_time(all[i], m_tiles(all[i])[0].second) * stages_of(all[i]) / split[i]; };
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost(a) > tile_cost(b); });
 
   plan->meta.clear();
@@ -469,17 +492,62 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   }
   const int T = (int)seq.size();
   if (T > (1 << 28)) return fail(MXMOE_GG_ERR_INVALID, "too many tiles (%d)", T);
+  auto tile_time = [&](const TileDesc& td) {
+    return stage_time(plan->meta[td.prob], td.cls & 0xFF) * (td.ks1 - td.ks0);
+  };
+  // chunks (in LPT order) to the least-loaded XCD queue; XCD x's i-th tile is block 8 i + x. A
+  // low-fill call's few long tiles would otherwise pile onto the first XCDs' round-robin chunks
+  // (bs=512: 40 % apart); full calls end up as before (every chunk costs about the same).
+  // Each XCD is simulated as `chunk` workgroup slots taking its queue's tiles in order (the
+  // hardware hands a freed slot the XCD's next block); a chunk joins the XCD whose simulated finish
+  // grows least (ties: least total time). The last 16 chunks' worth of tiles go in chunks of 4, so
+  // the finish times can even out to a tile or two.
   const int chunk = v.chunk;
-  const int nchunks = (T + chunk - 1) / chunk;
-  const int rounds = (nchunks + 7) / 8;
-  int grid = 0;
-  plan->tiles.assign((size_t)rounds * 8 * chunk, TileDesc{-1, 0, 0, 0, 0, 0, -1, -1});
-  for (int s = 0; s < T; ++s) {
-    const int c = s / chunk, pos = s % chunk;
-    const int b = 8 * (chunk * (c / 8) + pos) + (c % 8);
-    plan->tiles[b] = seq[s];
-    grid = std::max(grid, b + 1);
+  struct XcdSim {
+    std::vector<double> slot;  // min-heap of slot free times
+    double finish = 0, load = 0;
+    void add(double t) {
+      std::pop_heap(slot.begin(), slot.end(), std::greater<double>());
+      slot.back() += t;
+      finish = std::max(finish, slot.back());
+      std::push_heap(slot.begin(), slot.end(), std::greater<double>());
+      load += t;
+    }
+  };
+  std::vector<XcdSim> sim(8);
+  for (auto& x : sim) x.slot.assign(chunk, 0.0);
+  std::vector<std::vector<int>> queue(8);
+  const char* rr_env = getenv("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
+  const bool round_robin = rr_env && rr_env[0] == '1';
+  for (int s0 = 0, c = 0; s0 < T; ++c) {
+    const int len = (round_robin || T - s0 > 16 * chunk) ? chunk : std::min(chunk, 4);
+    const int s1 = std::min(T, s0 + len);
+    int best = c % 8;
+    if (!round_robin) {
+      XcdSim best_sim;
+      for (int x = 0; x < 8; ++x) {
+        XcdSim trial = sim[x];
+        for (int s = s0; s < s1; ++s) trial.add(tile_time(seq[s]));
+        if (x == 0 || trial.finish < best_sim.finish || (trial.finish == best_sim.finish && trial.load < best_sim.load)) {
+          best = x;
+          best_sim = std::move(trial);
+        }
+      }
+      sim[best] = std::move(best_sim);
+    }
+    for (int s = s0; s < s1; ++s) queue[best].push_back(s);
+    s0 = s1;
   }
+  size_t qmax = 0;
+  for (const auto& q : queue) qmax = std::max(qmax, q.size());
+  int grid = 0;
+  plan->tiles.assign(8 * qmax, TileDesc{-1, 0, 0, 0, 0, 0, -1, -1});
+  for (int x = 0; x < 8; ++x)
+    for (size_t i = 0; i < queue[x].size(); ++i) {
+      const int b = (int)(8 * i) + x;
+      plan->tiles[b] = seq[queue[x][i]];
+      grid = std::max(grid, b + 1);
+    }
   plan->tiles.resize(grid);
   plan->total_tiles = T;
   return MXMOE_GG_OK;
