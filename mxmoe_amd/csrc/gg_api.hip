@@ -78,6 +78,8 @@ template <int ABL>
 void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   if constexpr ((ABL & kAblMask) != 0) {
     launch_v2_q<ABL, 7>(a, grid, s);
+  } else if constexpr ((ABL & kWoAblMask) != 0) {
+    launch_v2_q<ABL, 8>(a, grid, s);  // weight-only ablations: w4a16 tiles only
   } else {
     switch (qmask & 63) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
@@ -194,6 +196,10 @@ const std::vector<Variant>& variants() {
       make_v2<ABL_B_TILED>("abl_v2_b_tiled"),
       // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB): AUTO for short-K calls
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
+      // weight-only timing ablations (WRONG RESULTS by design; w4a16 tiles only)
+      make_v2<V2_STAGGER | ABL_WO_BTILED>("abl_v2s_wo_btiled"),
+      make_v2<V2_STAGGER | ABL_WO_NODMA>("abl_v2s_wo_nodma"),
+      make_v2<V2_STAGGER | ABL_WO_NOCOMPUTE>("abl_v2s_wo_nocompute"),
   };
   return v;
 }

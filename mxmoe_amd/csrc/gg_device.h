@@ -506,8 +506,12 @@ enum : int {
   ABL_B_NODMA = 512,    // ablation: B operand never loaded (A only)
   ABL_B_REGLOAD = 1024,  // ablation: B operand loaded into registers (same global traffic), not into LDS
   ABL_B_TILED = 2048,    // ablation: B read as if stored in contiguous 32-KiB (256 rows x 128 B) stage blocks
-  V2_B3 = 4096           // stagger: B in a 3-stage LDS ring, two stages ahead (A: 2 stages, one ahead)
+  V2_B3 = 4096,          // stagger: B in a 3-stage LDS ring, two stages ahead (A: 2 stages, one ahead)
+  // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
+  // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
+  ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
 };
+constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
 
 // Tile timeline (diagnostics, V2_TRACE builds only): per block {start, mainloop end, end (stores
@@ -1432,7 +1436,7 @@ __device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uin
   return out;
 }
 
-template <class Cfg, int BITS>
+template <class Cfg, int BITS, int WABL = 0>
 __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SB,
                                            _Float16* __restrict__ C, int m0, int n0, uint8_t* lds, const SplitK& sk) {
@@ -1469,15 +1473,21 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       const int row = (wave * GBW + j) * RPI + lane / LPR;
       const int chunk = (lane % LPR) ^ ((row >> RSH) & (LPR - 1));  // source chunk for this LDS slot
       srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + chunk * 16;
+      if constexpr ((WABL & ABL_WO_BTILED) != 0)
+        srcB[j] = B + (int64_t)(n0 / Cfg::BN) * (mt.K / 64) * (Cfg::BN * RB) + row * RB + chunk * 16;
     }
   }
   auto issue = [&](int s, int buf) {
+    if constexpr ((WABL & ABL_WO_NODMA) != 0) {
+      if (s >= NBUF) return;
+    }
     uint8_t* As = lds + buf * SB_;
     uint8_t* Bs = As + Cfg::A_BYTES;
+    const int64_t boff = (WABL & ABL_WO_BTILED) ? (int64_t)(ks0 + s) * (Cfg::BN * RB) : (int64_t)(ks0 + s) * RB;
 #pragma unroll
     for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < GBW; ++j) glds16(srcB[j] + (ks0 + s) * RB, Bs + (wave * GBW + j) * 1024);
+    for (int j = 0; j < GBW; ++j) glds16(srcB[j] + boff, Bs + (wave * GBW + j) * 1024);
   };
 
   // per-lane columns and their scale / zp pairs (packed (x, x) halves for v_pk_fma_f16)
@@ -1573,7 +1583,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       const bool next_group = (ks0 + s + 1) % gstages == 0 && s + 1 < nst;
       if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
       if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
-      compute(s % NBUF);
+      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF);
       if (next_group) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -1630,9 +1640,10 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
     else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v2<V2Cfg<64>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
-    if (cls == 0) gg_tile_wo<WoCfg<256>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    else gg_tile_wo<WoCfg<64, 1>, 4>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    constexpr int WABL = ABL & kWoAblMask;
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_wo<WoCfg<64, 1>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
     if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
