@@ -117,8 +117,9 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
 
 /* The concrete variant `variant` (MXMOE_GG_VARIANT_AUTO or an index) resolves to for these
  * problems, written to *out. Host only (no GPU). AUTO: w4a4-only sets -> the 256x128 2-WG/CU
- * kernel (unless the plan needs split-K); calls whose median tile has <= 24 128-B K stages ->
- * the 3-stage-B-ring staggered kernel; otherwise mxmoe_gg_default_variant(). */
+ * kernel (unless the plan needs split-K); calls whose median tile has <= 24 128-B K stages, or
+ * whose tiles are mostly fp16 64-row remainders (small batches) -> the 3-stage-B-ring staggered
+ * kernel; otherwise mxmoe_gg_default_variant(). */
 int mxmoe_gg_resolve_variant(const mxmoe_gg_problem* problems, int problem_count, int variant, int* out);
 
 /* Device workspace bytes the plan of these problems needs with this variant

@@ -584,14 +584,21 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == 0) *out = variant_index(kInt4Variant);
   } else if (mask & ((1 << QT_F16) | (1 << QT_I8) | (1 << QT_I4))) {
     std::vector<std::pair<int, int64_t>> st;  // (128-B K stages, tiles) of the fp16 / w8a8 / w4a4 problems
-    int64_t total = 0;
+    int64_t total = 0, f16_small = 0;         // f16_small: fp16 tiles of the 64-row class
     for (const HostProblem& p : hp) {
       int qt;
       if (p.M <= 0 || qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) != MXMOE_GG_OK) continue;
       if (qt != QT_F16 && qt != QT_I8 && qt != QT_I4) continue;
-      const int64_t tiles = (int64_t)((p.M + 255) / 256) * ((p.N + 255) / 256);
+      const int64_t nt = (p.N + 255) / 256, tiles = (int64_t)((p.M + 255) / 256) * nt;
       st.emplace_back((int)(((int64_t)p.K * p.a_bits / 8 + 127) / 128), tiles);
       total += tiles;
+      if (qt == QT_F16 && p.M % 256 > 0 && p.M % 256 <= 64) f16_small += nt;
+    }
+    // low-fill fp16 calls (most tiles are 64-row remainders, e.g. bs=512 routed experts): those
+    // tiles wait on their B stream, and the deeper B ring pays (+5-9 %, session3/exp_b3_bs512.jsonl)
+    if (total > 0 && 2 * f16_small >= total) {
+      *out = variant_index(kShortKVariant);
+      return MXMOE_GG_OK;
     }
     std::sort(st.begin(), st.end());
     int64_t acc = 0;

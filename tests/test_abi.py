@@ -109,6 +109,9 @@ def test_auto_variant_short_k_rule():
         probs = [_prob(M=s.M, N=s.N, K=s.K, **f16) for s in layer[gg]]
         assert auto(probs) == want, gg
     assert auto([_prob(M=64, N=128, K=256)]) == nat.resolve_variant((nat.GGProblemC * 1)(_prob(M=64, N=128, K=256)), 1, b3)
+    # low-fill fp16 (bs=512: most tiles are 64-row remainders) -> the deep B ring even at long K
+    small = load_workload(qwen2_layer11_workload(512))["layer-11"]["gate_up"]
+    assert auto([_prob(M=s.M, N=s.N, K=s.K, **f16) for s in small]) == b3
 
 
 def _plan(problems, ws_bytes=1 << 20):
