@@ -1573,14 +1573,17 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
     for (int p = 0; p < DIST; ++p)
       if (p < nst) issue(p, p);
+    int gpos = (ks0 + 1) % gstages;  // (ks0 + s + 1) % gstages, kept as a counter (no divide per stage)
     for (int s = 0; s < nst; ++s) {
       // stages s+1 .. min(s+DIST-1, nst-1) were issued after s (younger scale loads only make the
-      // in-order count wait longer, never shorter)
-      wait_stage(min(DIST - 1, nst - 1 - s));
+      // in-order count wait longer, never shorter); the steady state is one constant wait
+      if (s + DIST - 1 < nst) wait_vmcnt<(DIST - 1) * DPS>();
+      else wait_stage(nst - 1 - s);
       lds_barrier();  // stage s visible to every wave; buffer (s-1) % NBUF released by all
       // next group's scales BEFORE this iteration's DMA: the wait the compiler places before their
       // use then leaves the (younger) DMA in flight instead of draining it
-      const bool next_group = (ks0 + s + 1) % gstages == 0 && s + 1 < nst;
+      const bool next_group = gpos == 0 && s + 1 < nst;
+      gpos = gpos + 1 == gstages ? 0 : gpos + 1;
       if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
       if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
       if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF);
