@@ -920,7 +920,10 @@ int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bi
     if (w_bits == 4) memset(o, 0, row_bytes);
     for (int k = 0; k < K; ++k) {
       const int seg = k / 64, kl = k % 64, kc = kl / 32, g = (kl % 32) / 8, e = kl % 8;
-      const size_t pos = (size_t)seg * 64 + g * 16 + kc * 8 + e;
+      // 4-bit: code e of a unit at nibble (e >> 1) | (e & 1) << 2, so codes 2q and 2q+1 are the
+      // nibbles at bits 4q and 16 + 4q of the unit's word (one v_and_or_b32 per fp16 pair)
+      const int ep = w_bits == 4 ? (e >> 1) | ((e & 1) << 2) : e;
+      const size_t pos = (size_t)seg * 64 + g * 16 + kc * 8 + ep;
       const uint8_t u = orig[(size_t)n * K + k];
       if (w_bits == 8) o[pos] = u;
       else o[pos / 2] |= (uint8_t)(u << (4 * (pos & 1)));

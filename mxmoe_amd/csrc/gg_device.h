@@ -1412,10 +1412,9 @@ template <int BITS>
 __device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uint32_t s2, uint32_t z2) {
   uint32_t d[4];
   if constexpr (BITS == 4) {
-    const uint32_t lo = w[0] & 0x0F0F0F0Fu, hi = (w[0] >> 4) & 0x0F0F0F0Fu;  // even / odd K codes
+    // repacked order: codes 2q, 2q+1 at bits 4q and 16 + 4q -> one v_and_or_b32 per fp16 pair
 #pragma unroll
-    for (int q = 0; q < 4; ++q)  // half pair q = (K 2q, K 2q+1): byte q of lo and of hi
-      d[q] = wo_perm(hi, lo, 0x0c040c00u + 0x00010001u * q) | 0x64006400u;
+    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (4 * q)) & 0x000F000Fu) | 0x64006400u;
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // bytes 2q, 2q+1 of the 8 codes

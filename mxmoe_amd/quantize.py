@@ -126,11 +126,13 @@ def quant_weightonly(w: torch.Tensor, bits: int, gsize: int, sym: bool) -> tuple
 
 def pack_weightonly_mi355x(codes: torch.Tensor, bits: int) -> torch.Tensor:
     """Stored codes uint8 [N, K] -> kernel layout uint8 [N, K * bits / 8]: in each 64-K segment the
-    K values {kc*32 + g*8 + e} sit at element position g*16 + kc*8 + e; 4-bit low nibble first."""
+    K values {kc*32 + g*8 + e} sit at element position g*16 + kc*8 + e (4-bit: e at nibble
+    (e >> 1) | (e & 1) << 2 of the unit, include/mxmoe_gg.h); 4-bit low nibble first."""
     N, K = codes.shape
     if K % 64:
         raise ValueError("weight-only needs K % 64 == 0")
-    u = codes.reshape(N, K // 64, 2, 4, 8).transpose(2, 3).reshape(N, K)
+    u = codes.reshape(N, K // 64, 2, 4, 8).transpose(2, 3)
     if bits == 8:
-        return u.contiguous()
+        return u.reshape(N, K).contiguous()
+    u = u[..., [0, 2, 4, 6, 1, 3, 5, 7]].reshape(N, K)
     return (u[:, 0::2] | (u[:, 1::2] << 4)).contiguous()

@@ -133,13 +133,14 @@ def ref_pack(q: np.ndarray, bits: int, sym: bool) -> np.ndarray:
 
 def mi355x_pack(q: np.ndarray, bits: int, sym: bool) -> np.ndarray:
     """The layout libmxmoe_gg consumes (include/mxmoe_gg.h): per 64-K segment of a row, unit g of
-    K values {kc*32 + g*8 + e} stored at element position g*16 + kc*8 + e; 4-bit: low nibble first."""
+    K values {kc*32 + g*8 + e} stored at element position g*16 + kc*8 + e; 4-bit: e at nibble
+    (e >> 1) | (e & 1) << 2 of the unit (codes 2q, 2q+1 at bits 4q, 16 + 4q), low nibble first."""
     N, K = q.shape
     u = stored_codes(q, bits, sym).astype(np.uint8).reshape(N, K // 64, 2, 4, 8).transpose(0, 1, 3, 2, 4)
-    u = u.reshape(N, K)
     if bits == 8:
-        return np.ascontiguousarray(u)
+        return np.ascontiguousarray(u.reshape(N, K))
     assert bits == 4
+    u = u[..., [0, 2, 4, 6, 1, 3, 5, 7]].reshape(N, K)
     return (u[:, 0::2] | (u[:, 1::2] << 4)).astype(np.uint8)
 
 
