@@ -467,8 +467,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     return std::max(bytes, equiv) + 24576.0;
   };
   // problems by the modelled time of their first (tallest) tile, longest first
-  auto tile_cost = [&](int i) { return stage_time(all[i], m_tiles(all[i])[0].second) * stages_of(all[i]) / split[i]; };
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost(a) > tile_cost(b); });
+  std::vector<double> tile_cost(P, 0.0);
+  for (int i : order) tile_cost[i] = stage_time(all[i], m_tiles(all[i])[0].second) * stages_of(all[i]) / split[i];
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost[a] > tile_cost[b]; });
 
   plan->meta.clear();
   plan->order = order;
@@ -526,22 +527,32 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   const char* rr_env = getenv("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
   const bool round_robin = rr_env && rr_env[0] == '1';
   for (int s0 = 0, c = 0; s0 < T; ++c) {
-    const int len = (round_robin || T - s0 > 16 * chunk) ? chunk : std::min(chunk, 4);
+    const bool head = T - s0 > 16 * chunk;
+    const int len = (round_robin || head) ? chunk : std::min(chunk, 4);
     const int s1 = std::min(T, s0 + len);
+    double times[64];
+    for (int s = s0; s < s1; ++s) times[s - s0] = tile_time(seq[s]);
     int best = c % 8;
-    if (!round_robin) {
-      XcdSim best_sim;
+    if (!round_robin && head) {  // full chunks: least total time (cheap; the tail evens out)
+      best = 0;
+      for (int x = 1; x < 8; ++x)
+        if (sim[x].load < sim[best].load) best = x;
+    } else if (!round_robin) {  // tail: least simulated finish
+      double best_finish = 0, best_load = 0;
       for (int x = 0; x < 8; ++x) {
         XcdSim trial = sim[x];
-        for (int s = s0; s < s1; ++s) trial.add(tile_time(seq[s]));
-        if (x == 0 || trial.finish < best_sim.finish || (trial.finish == best_sim.finish && trial.load < best_sim.load)) {
+        for (int s = s0; s < s1; ++s) trial.add(times[s - s0]);
+        if (x == 0 || trial.finish < best_finish || (trial.finish == best_finish && trial.load < best_load)) {
           best = x;
-          best_sim = std::move(trial);
+          best_finish = trial.finish;
+          best_load = trial.load;
         }
       }
-      sim[best] = std::move(best_sim);
     }
-    for (int s = s0; s < s1; ++s) queue[best].push_back(s);
+    for (int s = s0; s < s1; ++s) {
+      sim[best].add(times[s - s0]);
+      queue[best].push_back(s);
+    }
     s0 = s1;
   }
   size_t qmax = 0;
