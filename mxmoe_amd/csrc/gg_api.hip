@@ -471,6 +471,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   for (int i : order) tile_cost[i] = stage_time(all[i], m_tiles(all[i])[0].second) * stages_of(all[i]) / split[i];
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost[a] > tile_cost[b]; });
 
+  // m-tiles per band (n-major inside a band): a 32-tile chunk is band x (32 / band) tiles
+  const char* band_env = getenv("MXMOE_GG_BAND");  // A/B switch (default 4)
+  const size_t band = band_env && atoi(band_env) > 0 ? (size_t)atoi(band_env) : 4;
   plan->meta.clear();
   plan->order = order;
   plan->slabs = 0;
@@ -482,9 +485,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     const std::vector<std::pair<int, int>> mt = m_tiles(m);  // (m0, cls)
     m.tile_begin = (int32_t)seq.size();
     const int nt = m.tiles_n, S = split[order[row]], nst = stages_of(m);
-    for (size_t mb = 0; mb < mt.size(); mb += 4)
+    for (size_t mb = 0; mb < mt.size(); mb += band)
       for (int n = 0; n < nt; ++n)
-        for (size_t mi = mb; mi < std::min(mt.size(), mb + 4); ++mi) {
+        for (size_t mi = mb; mi < std::min(mt.size(), mb + band); ++mi) {
           if (S == 1) {
             seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second, 0, nst, -1, -1});
             continue;
