@@ -505,13 +505,12 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   auto tile_time = [&](const TileDesc& td) {
     return stage_time(plan->meta[td.prob], td.cls & 0xFF) * (td.ks1 - td.ks0);
   };
-  // chunks (in LPT order) to the least-loaded XCD queue; XCD x's i-th tile is block 8 i + x. A
-  // low-fill call's few long tiles would otherwise pile onto the first XCDs' round-robin chunks
-  // (bs=512: 40 % apart); full calls end up as before (every chunk costs about the same).
-  // Each XCD is simulated as `chunk` workgroup slots taking its queue's tiles in order (the
-  // hardware hands a freed slot the XCD's next block); a chunk joins the XCD whose simulated finish
-  // grows least (ties: least total time). The last 16 chunks' worth of tiles go in chunks of 4, so
-  // the finish times can even out to a tile or two.
+  // XCD queues (XCD x's i-th tile is block 8 i + x). Chunks in LPT order: full chunks join the
+  // XCD queue with the least modelled time; the last 16 chunks' worth of tiles go in chunks of
+  // `tail_chunk`, each to the XCD whose simulated finish grows least (ties: least total time) —
+  // every XCD simulated as `chunk` workgroup slots taking its queue in order, as the hardware
+  // hands a freed slot the XCD's next block. Plain round-robin chunks let a low-fill call's few
+  // long tiles pile onto 2-3 XCDs (bs=512: per-XCD busy time 40 % apart).
   const int chunk = v.chunk;
   struct XcdSim {
     std::vector<double> slot;  // min-heap of slot free times
@@ -527,11 +526,13 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   std::vector<XcdSim> sim(8);
   for (auto& x : sim) x.slot.assign(chunk, 0.0);
   std::vector<std::vector<int>> queue(8);
+  const char* tc_env = getenv("MXMOE_GG_TAIL_CHUNK");  // A/B switch: tail chunk size (default 16)
+  const int tail_chunk = tc_env && atoi(tc_env) > 0 ? atoi(tc_env) : 16;
   const char* rr_env = getenv("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
   const bool round_robin = rr_env && rr_env[0] == '1';
   for (int s0 = 0, c = 0; s0 < T; ++c) {
     const bool head = T - s0 > 16 * chunk;
-    const int len = (round_robin || head) ? chunk : std::min(chunk, 4);
+    const int len = (round_robin || head) ? chunk : std::min(chunk, tail_chunk);
     const int s1 = std::min(T, s0 + len);
     double times[64];
     for (int s = s0; s < s1; ++s) times[s - s0] = tile_time(seq[s]);
