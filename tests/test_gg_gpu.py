@@ -166,14 +166,19 @@ def test_nslice_views_match_full_call():
                 assert torch.equal(p.C.view(torch.int16), r.view(torch.int16)), (world, i)
 
 
+B3 = [ln.split()[1] for ln in nat.list_variants()].index("v2s3_256x256_w8_dma_stagger_bring3")
+
+
+@pytest.mark.parametrize("variant", [None, B3], ids=["auto", "v2s3"])
 @pytest.mark.parametrize("q", [FP16, W8A8, W4A4, QParams(16, 4, 128, False)], ids=["fp16", "w8a8", "w4a4", "w4a16g128"])
-def test_splitk_long_k_low_fill(q):
+def test_splitk_long_k_low_fill(q, variant):
     """Low-fill calls with a long K (the shared expert's down at small batch) are split along K;
     the last slice reduces the partial slabs in slice order: int paths stay bit-exact, results
-    are deterministic, and the arrival counters reset for the next launch."""
+    are deterministic, and the arrival counters reset for the next launch. Also with the 3-stage
+    B ring forced (its mainloop feeds the same split-K hand-off)."""
     specs = [(512, 2048, 5632), (40, 2048, 1408), (3, 256, 1408)]
     hps = [HostProblem(M, N, K, q, seed=90 + i, device=DEV) for i, (M, N, K) in enumerate(specs)]
-    gg = GroupGemm([h.problem for h in hps])
+    gg = GroupGemm([h.problem for h in hps], variant=variant)
     assert gg.info.splitk_slabs > 0
     gg.launch()
     torch.cuda.synchronize()
