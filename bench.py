@@ -48,6 +48,10 @@ CONFIGS = {
                   name="qwen2_moe layer-11 w4a16_g128_asym GroupGEMM bs=8192"),
     "w4a16_bs512": dict(kw=dict(qstr="w4a16_g128_asym"), peak="fp16", dtype="fp16 (int4 weights)", bs=512,
                         name="qwen2_moe layer-11 w4a16_g128_asym GroupGEMM bs=512 (weight-bandwidth bound)"),
+    "w2a16": dict(kw=dict(qstr="w2a16_g128_asym"), peak="fp16", dtype="fp16 (int2 weights)",
+                  name="qwen2_moe layer-11 w2a16_g128_asym GroupGEMM bs=8192"),
+    "w2a16_bs512": dict(kw=dict(qstr="w2a16_g128_asym"), peak="fp16", dtype="fp16 (int2 weights)", bs=512,
+                        name="qwen2_moe layer-11 w2a16_g128_asym GroupGEMM bs=512 (weight-bandwidth bound)"),
     "fp16_bs512": dict(kw={}, peak="fp16", dtype="fp16", bs=512,
                        name="qwen2_moe layer-11 fp16 GroupGEMM bs=512"),
 }

@@ -155,8 +155,10 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
  * sym codes stored with the +2^(w_bits-1)-1 offset) into the layout the kernels read:
  * uint8 [N][K * w_bits / 8], per 64-K segment of a row the K values {kc*32 + g*8 + e} at element
  * position g*16 + kc*8 + e (kc < 2, g < 4, e < 8); 4-bit: e at nibble (e >> 1) | (e & 1) << 2 of
- * the unit's 32-bit word (codes 2q, 2q+1 at bits 4q and 16 + 4q), low nibble first. Code values are
- * unchanged. Needs N % (8 * 16 / w_bits) == 0 and K % 64 == 0; w_bits 4 or 8. The scale / zero
+ * the unit's 32-bit word (codes 2q, 2q+1 at bits 4q and 16 + 4q), low nibble first; 2-bit: the
+ * unit (g) of a segment's 16-B row is one little-endian 32-bit word at byte 4 g holding both K
+ * halves, code (kc, e) at bit 16 (e & 1) + 2 (4 kc + e / 2). Code values are
+ * unchanged. Needs N % (8 * 16 / w_bits) == 0 and K % 64 == 0; w_bits 2, 4 or 8. The scale / zero
  * buffer is used as the reference lays it out (permute_scale: [K/gsize][N] sym, [K/gsize][N][2]
  * scale/zp pairs asym). */
 int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bits, uint8_t* out);

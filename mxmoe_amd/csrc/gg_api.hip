@@ -81,7 +81,7 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   } else if constexpr ((ABL & kWoAblMask) != 0) {
     launch_v2_q<ABL, 8>(a, grid, s);  // weight-only ablations: w4a16 tiles only
   } else {
-    switch (qmask & 63) {
+    switch (qmask & 127) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
       case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
       case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
@@ -90,9 +90,15 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       case 8: launch_v2_q<ABL, 8>(a, grid, s); break;    // w4a16 only
       case 16: launch_v2_q<ABL, 16>(a, grid, s); break;  // w8a16 only
       case 32: launch_v2_q<ABL, 32>(a, grid, s); break;  // w4a4 g128 only
+      case 64: launch_v2_q<ABL, 64>(a, grid, s); break;  // w2a16 only
       // any other mix: every tile body in one kernel. The staggered int bodies leave no register
-      // room for that (the compiler spilled inside their K loops), so the fallback is plain v2.
-      default: launch_v2_q<0, 63>(a, grid, s); break;
+      // room for that (the compiler spilled inside their K loops), so the fallback is plain v2;
+      // the 2-bit weight-only body only joins it when the mix has one (it costs 12 B of prologue
+      // spill there, tests/test_codegen.py)
+      default:
+        if (qmask & (1 << QT_W2A16)) launch_v2_q<0, 127>(a, grid, s);
+        else launch_v2_q<0, 63>(a, grid, s);
+        break;
     }
   }
 }
@@ -121,7 +127,7 @@ Variant make_v0(const char* name) {
   v.geom[QT_F16] = {C16::BM, C16::BN, C16::BKB, C16::kThreads};
   v.geom[QT_I8] = {C8::BM, C8::BN, C8::BKB, C8::kThreads};
   v.geom[QT_I4] = {C4::BM, C4::BN, C4::BKB, C4::kThreads};
-  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = {0, 0, 0, 0};  // v2 kernels only
+  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = v.geom[QT_W2A16] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = C16::kThreads;
   v.lds_bytes = FusedCfg<C16, C8, C4>::LDS_BYTES;
   v.chunk = FusedCfg<C16, C8, C4>::LDS_BYTES <= 80 * 1024 ? 64 : 32;  // workgroups per XCD at once
@@ -138,7 +144,7 @@ Variant make_v3(const char* name) {
   v.name = name;
   v.kind = Kind::V3;
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};
-  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = {0, 0, 0, 0};  // v2 kernels only
+  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = v.geom[QT_W2A16] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = CT::NT;
   v.lds_bytes = CT::LDS_BYTES;
   v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
@@ -156,6 +162,7 @@ Variant make_v2(const char* name) {
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, 256, 128, 512};
   v.geom[QT_W4A16] = {256, 256, 32, 512};  // 64-K stages: 32 B of 4-bit codes per row
   v.geom[QT_W8A16] = {256, 256, 64, 512};
+  v.geom[QT_W2A16] = {256, 256, 16, 512};  // 64-K stages: 16 B of 2-bit codes per row
   v.geom[QT_I4G] = {256, 256, 128, 512};  // w4a4 g128 (gg_tile_g128): 256 / 128-row classes as int4
   v.threads = 512;
   v.lds_bytes = (ABL & V2_B3) ? 160 * 1024 : V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA;
@@ -239,13 +246,15 @@ int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
     *qt = QT_I4G;
     return MXMOE_GG_OK;
   }
-  if (a_bits == 16 && (w_bits == 4 || w_bits == 8)) {  // weight-only; group size checked per problem
-    *qt = w_bits == 4 ? QT_W4A16 : QT_W8A16;
+  if (a_bits == 16 && (w_bits == 2 || w_bits == 4 || w_bits == 8)) {  // weight-only; group size checked per problem
+    *qt = w_bits == 2 ? QT_W2A16 : w_bits == 4 ? QT_W4A16 : QT_W8A16;
     return MXMOE_GG_OK;
   }
   return fail(MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported: w%da%d_g%d_%s", w_bits, a_bits, gsize,
               sym ? "sym" : "asym");
 }
+
+bool is_weightonly(int qt) { return qt == QT_W4A16 || qt == QT_W8A16 || qt == QT_W2A16; }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -320,7 +329,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (v.geom[qt].bn == 0)
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s does not implement w%da%d (quant type not supported)",
                 idx, v.name, p.w_bits, p.a_bits);
-  if (qt == QT_W4A16 || qt == QT_W8A16) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
+  if (is_weightonly(qt)) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
   const int abits = qt == QT_F16 ? 16 : p.a_bits;
   const int64_t kbits = (int64_t)p.K * abits;
   if (kbits % 128 != 0)
@@ -393,7 +402,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     if (probs[i].M > 0 && probs[i].N > 0) order.push_back(i);
   // K stages of a problem in its tile body (v2: 128 B per stage; weight-only: 64 elements)
   auto stages_of = [&](const GGMeta& m) {
-    if (m.qtype == QT_W4A16 || m.qtype == QT_W8A16) return m.K / 64;
+    if (is_weightonly(m.qtype)) return m.K / 64;
     return (m.kbytes + v.geom[m.qtype].bkb - 1) / v.geom[m.qtype].bkb;
   };
   auto full_tile_cost = [&](int i) {
@@ -409,7 +418,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     std::vector<std::pair<int, int>> mt;
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
-      const bool small_class = m.qtype == QT_F16 || m.qtype == QT_W4A16 || m.qtype == QT_W8A16;
+      const bool small_class = m.qtype == QT_F16 || is_weightonly(m.qtype);
       if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
         mt.push_back({m0, 2});
         m0 += v.tail2_bm;
@@ -455,8 +464,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     const TileGeom& g = v.geom[m.qtype];
     const double rows = class_rows(cls, g), cols = g.bn;
     double bytes, equiv;
-    if (m.qtype == QT_W4A16 || m.qtype == QT_W8A16) {  // 64 K elements per stage, fp16 A
-      bytes = rows * 128 + cols * 64 * (m.qtype == QT_W4A16 ? 4 : 8) / 8.0;
+    if (is_weightonly(m.qtype)) {  // 64 K elements per stage, fp16 A
+      bytes = rows * 128 + cols * 64 * (m.qtype == QT_W2A16 ? 2 : m.qtype == QT_W4A16 ? 4 : 8) / 8.0;
       equiv = 2.0 * rows * cols * 64 / 128;
     } else {
       const double kel = g.bkb * 8.0 / (m.qtype == QT_F16 ? 16 : m.qtype == QT_I8 ? 8 : 4);
@@ -689,8 +698,8 @@ int mxmoe_gg_default_variant(void) { return variant_index(kDefaultVariantName); 
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
   // weight-only kernels cover every group size / sym of a bit width: listed under the base name
-  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16", "w8a16", "w4a4_g128_sym"};
-  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4};
+  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16", "w8a16", "w4a4_g128_sym", "w2a16"};
+  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4, 2};
   std::string out;
   const auto& vs = variants();
   for (size_t i = 0; i < vs.size(); ++i) {
@@ -886,8 +895,8 @@ int mxmoe_gg_debug_trace(void* dst, size_t bytes, int reset) {
 int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bits, uint8_t* out) {
   if (!ref_words || !out || N <= 0 || K <= 0)
     return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_repack_weightonly");
-  if (w_bits != 4 && w_bits != 8)
-    return fail(MXMOE_GG_ERR_UNSUPPORTED, "weight-only repack: w_bits must be 4 or 8 (got %d)", w_bits);
+  if (w_bits != 2 && w_bits != 4 && w_bits != 8)
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "weight-only repack: w_bits must be 2, 4 or 8 (got %d)", w_bits);
   const int pack = 16 / w_bits, mask = (1 << w_bits) - 1;
   if (N % (pack * 8) || K % 64)
     return fail(MXMOE_GG_ERR_INVALID, "weight-only repack: need N %% %d == 0 and K %% 64 == 0 (N=%d, K=%d)",
@@ -909,10 +918,15 @@ int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bi
     static const int p8[4] = {1, 0, 3, 2}, d8[8] = {0, 2, 4, 6, 1, 3, 5, 7};
     static const int p4[8] = {3, 7, 2, 6, 1, 5, 0, 4};
     static const int d4[16] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+    static const int p2[16] = {7, 15, 6, 14, 5, 13, 4, 12, 3, 11, 2, 10, 1, 9, 0, 8};  // quantize.cuh:343-347
+    static const int d2[32] = {0, 8,  16, 24, 1, 9,  17, 25, 2, 10, 18, 26, 3, 11, 19, 27,
+                               4, 12, 20, 28, 5, 13, 21, 29, 6, 14, 22, 30, 7, 15, 23, 31};
     if (w_bits == 8) {
       proj = p8, desired = d8, plen = 4;
-    } else {
+    } else if (w_bits == 4) {
       proj = p4, desired = d4, plen = 8;
+    } else {
+      proj = p2, desired = d2, plen = 16;
     }
     for (int i = 0; i < 4 * pack; i += plen)
       for (int j = 0; j < plen; ++j) perm[proj[j] + i] = desired[i + j];
@@ -932,7 +946,7 @@ int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bi
   const size_t row_bytes = (size_t)K * w_bits / 8;
   for (int n = 0; n < N; ++n) {
     uint8_t* o = out + (size_t)n * row_bytes;
-    if (w_bits == 4) memset(o, 0, row_bytes);
+    if (w_bits < 8) memset(o, 0, row_bytes);
     for (int k = 0; k < K; ++k) {
       const int seg = k / 64, kl = k % 64, kc = kl / 32, g = (kl % 32) / 8, e = kl % 8;
       // 4-bit: code e of a unit at nibble (e >> 1) | (e & 1) << 2, so codes 2q and 2q+1 are the
@@ -940,8 +954,16 @@ int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bi
       const int ep = w_bits == 4 ? (e >> 1) | ((e & 1) << 2) : e;
       const size_t pos = (size_t)seg * 64 + g * 16 + kc * 8 + ep;
       const uint8_t u = orig[(size_t)n * K + k];
-      if (w_bits == 8) o[pos] = u;
-      else o[pos / 2] |= (uint8_t)(u << (4 * (pos & 1)));
+      if (w_bits == 8) {
+        o[pos] = u;
+      } else if (w_bits == 4) {
+        o[pos / 2] |= (uint8_t)(u << (4 * (pos & 1)));
+      } else {
+        // 2-bit: the unit (seg, g) is one 32-bit word holding both K halves; code (kc, e) at bit
+        // 2 (4 kc + e / 2) for even e and 16 + 2 (4 kc + e / 2) for odd e (fp16 pairs, one and_or)
+        const int bit = (e & 1) * 16 + 2 * (4 * kc + e / 2);
+        o[(size_t)seg * 16 + g * 4 + bit / 8] |= (uint8_t)(u << (bit % 8));
+      }
     }
   }
   return MXMOE_GG_OK;

@@ -32,7 +32,7 @@
 namespace mxmoe {
 
 // QT_I4G: w4a4_g128_sym (A and B int4 with one fp16 scale per 128-K group)
-enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_I4G = 5, QT_COUNT = 6 };
+enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_I4G = 5, QT_W2A16 = 6, QT_COUNT = 7 };
 
 // One row of the plan table (64 B), written by the host planner into the workspace.
 struct GGMeta {
@@ -1415,6 +1415,10 @@ __device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uin
     // repacked order: codes 2q, 2q+1 at bits 4q and 16 + 4q -> one v_and_or_b32 per fp16 pair
 #pragma unroll
     for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (4 * q)) & 0x000F000Fu) | 0x64006400u;
+  } else if constexpr (BITS == 2) {
+    // w[0] = the unit's 32-bit word pre-shifted by 8 * kc: codes 2q, 2q+1 at bits 2q and 16 + 2q
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (2 * q)) & 0x00030003u) | 0x64006400u;
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // bytes 2q, 2q+1 of the 8 codes
@@ -1441,7 +1445,10 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
                                            _Float16* __restrict__ C, int m0, int n0, uint8_t* lds, const SplitK& sk) {
   constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA;
   constexpr int RB = Cfg::KS * BITS / 8;        // B bytes per row per stage
-  constexpr int LPR = RB / 16, RPI = 64 / LPR;  // lanes per B row, B rows per wave-instruction
+  // B DMA granule per lane: 16 B, or 4 B for 2-bit codes (16-B rows: 4 lanes per row, so every
+  // wave still issues whole instructions and the vmcnt bookkeeping stays uniform)
+  constexpr int GRAN = BITS == 2 ? 4 : 16;
+  constexpr int LPR = RB / GRAN, RPI = 64 / LPR;  // lanes per B row, B rows per wave-instruction
   // B chunk swizzle: the 16-B chunk c of tile row n sits in LDS slot c ^ ((n >> RSH) & (LPR - 1)),
   // RSH = log2(rows per 256-B bank window); rows n, n + 256 / RB then hit different banks
   constexpr int RSH = BITS == 4 ? 3 : 2;
@@ -1470,10 +1477,11 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
     for (int j = 0; j < GBW; ++j) {
       const int row = (wave * GBW + j) * RPI + lane / LPR;
-      const int chunk = (lane % LPR) ^ ((row >> RSH) & (LPR - 1));  // source chunk for this LDS slot
-      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + chunk * 16;
+      // source chunk for this LDS slot (2-bit: 4-B granules, rows unswizzled)
+      const int chunk = BITS == 2 ? lane % LPR : (lane % LPR) ^ ((row >> RSH) & (LPR - 1));
+      srcB[j] = B + (int64_t)min(n0 + row, N - 1) * ldb + chunk * GRAN;
       if constexpr ((WABL & ABL_WO_BTILED) != 0)
-        srcB[j] = B + (int64_t)(n0 / Cfg::BN) * (mt.K / 64) * (Cfg::BN * RB) + row * RB + chunk * 16;
+        srcB[j] = B + (int64_t)(n0 / Cfg::BN) * (mt.K / 64) * (Cfg::BN * RB) + row * RB + chunk * GRAN;
     }
   }
   auto issue = [&](int s, int buf) {
@@ -1486,13 +1494,18 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
     for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < GBW; ++j) glds16(srcB[j] + boff, Bs + (wave * GBW + j) * 1024);
+    for (int j = 0; j < GBW; ++j) {
+      if constexpr (BITS == 2)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[j] + boff), (lds_void_t*)(Bs + (wave * GBW + j) * 256), 4, 0, 0);
+      else
+        glds16(srcB[j] + boff, Bs + (wave * GBW + j) * 1024);
+    }
   };
 
   // per-lane columns and their scale / zp pairs (packed (x, x) halves for v_pk_fma_f16)
   const int ncol0 = n0 + wn * Cfg::WTN;
   // fp16 -(1024 + off) = 0xE400 | off: sym off = 7 (4-bit) / 127 (8-bit), asym 0
-  const uint32_t moff2 = sym ? (BITS == 4 ? 0xE407E407u : 0xE47FE47Fu) : 0xE400E400u;
+  const uint32_t moff2 = sym ? (BITS == 4 ? 0xE407E407u : BITS == 2 ? 0xE401E401u : 0xE47FE47Fu) : 0xE400E400u;
   uint32_t s2[FN], z2[FN], s2n[FN], z2n[FN];  // current group, next group (prefetched)
   auto load_scales = [&](int grp, uint32_t (&so)[FN], uint32_t (&zo)[FN]) {
 #pragma unroll
@@ -1525,6 +1538,10 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     const uint8_t* As = lds + buf * SB_ + a_row;
     const uint8_t* Bs = lds + buf * SB_ + Cfg::A_BYTES + b_row;
     uint32_t raw[FN][2];  // 4-bit: the codes of both K halves (one 8-B read); 8-bit: one K half
+    if constexpr (BITS == 2) {  // 2-bit: both K halves in one 4-B word (unit g of the 16-B row)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) raw[j][0] = *reinterpret_cast<const uint32_t*>(Bs + j * 16 * RB + g * 4);
+    }
     if constexpr (BITS == 4) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -1539,7 +1556,10 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       v8h b[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        if constexpr (BITS == 4) {
+        if constexpr (BITS == 2) {
+          const uint32_t w = raw[j][0] >> (8 * kc);
+          b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j]);
+        } else if constexpr (BITS == 4) {
           b[j] = wo_dequant<4>(&raw[j][kc], moff2, s2[j], z2[j]);
         } else {
           const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + ((g ^ bsw) << 4) + kc * 8);
@@ -1650,6 +1670,10 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
     if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_wo<WoCfg<64, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  } else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) {
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 2>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 2>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_wo<WoCfg<64, 1>, 2>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   }
   if constexpr ((ABL & V2_TRACE) != 0) {
     if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) {

@@ -60,15 +60,17 @@ FP16 = QParams()
 W8A8 = QParams(8, 8, -1, True)
 W4A4 = QParams(4, 4, -1, True)
 W4A4_G128 = QParams(4, 4, 128, True)  # w4a4_g128_sym: one scale per 128-K group (cta_gemm.cuh:610-772)
-# weight-only (any group size that is -1 or a multiple of 64 dividing K, sym or asym, 4 / 8 bits)
+# weight-only (any group size that is -1 or a multiple of 64 dividing K, sym or asym, 2 / 4 / 8 bits)
 W4A16_G128_ASYM = QParams(16, 4, 128, False)
 W4A16_ASYM = QParams(16, 4, -1, False)
 W4A16_G128_SYM = QParams(16, 4, 128, True)
 W8A16_ASYM = QParams(16, 8, -1, False)
+W2A16_G128_ASYM = QParams(16, 2, 128, False)
 
 SUPPORTED = {q.qcfg: q for q in (FP16, W8A8, W4A4, W4A4_G128, W4A16_G128_ASYM, W4A16_ASYM, W4A16_G128_SYM, W8A16_ASYM,
                                   QParams(16, 4, -1, True), QParams(16, 8, -1, True), QParams(16, 8, 128, True),
-                                  QParams(16, 8, 128, False))}
+                                  QParams(16, 8, 128, False), W2A16_G128_ASYM, QParams(16, 2, -1, False),
+                                  QParams(16, 2, -1, True), QParams(16, 2, 128, True))}
 
 
 @dataclasses.dataclass

@@ -97,8 +97,8 @@ def quant_weightonly(w: torch.Tensor, bits: int, gsize: int, sym: bool) -> tuple
     """fp16 [N, K] -> (stored codes uint8 [N, K], scale_zp fp16 flat: sym [G][N], asym [G][N][2])."""
     if w.dtype != torch.float16:
         raise TypeError("quant_weightonly expects fp16 input (the reference quantises in half)")
-    if bits not in (4, 8):
-        raise ValueError("weight-only: 4 / 8-bit codes")
+    if bits not in (2, 4, 8):
+        raise ValueError("weight-only: 2 / 4 / 8-bit codes")
     N, K = w.shape
     g = K if gsize == -1 else gsize
     if K % g:
@@ -127,10 +127,17 @@ def quant_weightonly(w: torch.Tensor, bits: int, gsize: int, sym: bool) -> tuple
 def pack_weightonly_mi355x(codes: torch.Tensor, bits: int) -> torch.Tensor:
     """Stored codes uint8 [N, K] -> kernel layout uint8 [N, K * bits / 8]: in each 64-K segment the
     K values {kc*32 + g*8 + e} sit at element position g*16 + kc*8 + e (4-bit: e at nibble
-    (e >> 1) | (e & 1) << 2 of the unit, include/mxmoe_gg.h); 4-bit low nibble first."""
+    (e >> 1) | (e & 1) << 2 of the unit, include/mxmoe_gg.h); 4-bit low nibble first; 2-bit: the
+    unit's 16 codes in one little-endian 32-bit word."""
     N, K = codes.shape
     if K % 64:
         raise ValueError("weight-only needs K % 64 == 0")
+    if bits == 2:  # unit (seg, g) = one 32-bit word: code (kc, e) at bit 16 (e & 1) + 2 (4 kc + e // 2)
+        e = torch.arange(8)
+        shift = ((e % 2) * 16)[None, :] + 2 * (4 * torch.arange(2)[:, None] + e[None, :] // 2)
+        u = codes.reshape(N, K // 64, 2, 4, 8).to(torch.int64).transpose(2, 3)  # [N, seg, g, kc, e]
+        word = (u << shift.to(codes.device)).sum(dim=(-2, -1)).to(torch.int32)  # [N, seg, g]
+        return word.contiguous().view(torch.uint8).reshape(N, K // 4)
     u = codes.reshape(N, K // 64, 2, 4, 8).transpose(2, 3)
     if bits == 8:
         return u.reshape(N, K).contiguous()

@@ -29,9 +29,9 @@ SUPPORTED_QCFG = [
       for ty in ["", "_accfp16", "_bf16"]],
 ]
 
-# what the MI355X kernels implement (2-bit weight-only, bf16 / fp8 and the _accfp16 forms are not built)
+# what the MI355X kernels implement (bf16 / fp8 and the _accfp16 forms are not built)
 MI355X_QCFG = ["fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a4_g128_sym",
-               *[f"w{w}a16_g{g}_{s}" for w in (4, 8) for g in (-1, 128) for s in ("sym", "asym")]]
+               *[f"w{w}a16_g{g}_{s}" for w in (4, 8, 2) for g in (-1, 128) for s in ("sym", "asym")]]
 
 
 def get_info_from_qcfg_str(qcfg: str) -> tuple[int, int, int, bool]:

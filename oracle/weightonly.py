@@ -137,6 +137,11 @@ def mi355x_pack(q: np.ndarray, bits: int, sym: bool) -> np.ndarray:
     (e >> 1) | (e & 1) << 2 of the unit (codes 2q, 2q+1 at bits 4q, 16 + 4q), low nibble first."""
     N, K = q.shape
     u = stored_codes(q, bits, sym).astype(np.uint8).reshape(N, K // 64, 2, 4, 8).transpose(0, 1, 3, 2, 4)
+    if bits == 2:  # unit (seg, g): one little-endian 32-bit word, code (kc, e) at bit 16 (e&1) + 2 (4 kc + e//2)
+        kc, e = np.meshgrid(np.arange(2), np.arange(8), indexing="ij")
+        shift = (e % 2) * 16 + 2 * (4 * kc + e // 2)
+        word = (u.astype(np.uint64) << shift.astype(np.uint64)).sum(axis=(-2, -1)).astype(np.uint32)
+        return np.ascontiguousarray(word).view(np.uint8).reshape(N, K // 4)
     if bits == 8:
         return np.ascontiguousarray(u.reshape(N, K))
     assert bits == 4

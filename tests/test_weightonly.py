@@ -13,7 +13,7 @@ from mxmoe_amd.quantize import pack_weightonly_mi355x, quant_weightonly
 from oracle import weightonly as wo
 
 
-@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("bits", [2, 4, 8])
 @pytest.mark.parametrize("sym", [True, False])
 @pytest.mark.parametrize("N,K", [(64, 128), (256, 1408), (96, 64)])
 def test_repack_inverts_reference_packing(bits, sym, N, K):
@@ -34,7 +34,8 @@ def test_reference_permutation_is_a_bijection():
 
 
 @pytest.mark.parametrize("args,status", [
-    ((64, 128, 2), nat.MXMOE_GG_ERR_UNSUPPORTED),
+    ((64, 128, 3), nat.MXMOE_GG_ERR_UNSUPPORTED),
+    ((32, 128, 2), nat.MXMOE_GG_ERR_INVALID),  # 2-bit: N % 64
     ((60, 128, 4), nat.MXMOE_GG_ERR_INVALID),
     ((64, 96, 4), nat.MXMOE_GG_ERR_INVALID),
 ])
@@ -45,7 +46,7 @@ def test_repack_rejects_bad_shapes(args, status):
     assert nat.lib().mxmoe_gg_repack_weightonly(src.ctypes.data, N, K, bits, out.ctypes.data) == status
 
 
-@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("bits", [2, 4, 8])
 @pytest.mark.parametrize("gsize", [-1, 128])
 @pytest.mark.parametrize("sym", [True, False])
 def test_torch_quantisation_matches_oracle(bits, gsize, sym):
@@ -86,7 +87,7 @@ def _variant(name):
     (dict(gsize=128, K=192), nat.MXMOE_GG_ERR_UNSUPPORTED, "group size"),
     (dict(scale_b=0), nat.MXMOE_GG_ERR_INVALID, "NULL scale"),
     (dict(scale_b=18), nat.MXMOE_GG_ERR_INVALID, "4-byte aligned"),
-    (dict(w_bits=2), nat.MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported"),
+    (dict(w_bits=3), nat.MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported"),
 ])
 def test_weightonly_validation(kw, status, msg):
     st, err = _plan([_prob(), _prob(**kw)], nat.default_variant())

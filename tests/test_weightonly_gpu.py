@@ -11,7 +11,7 @@ from tests._util import HostProblem, assert_f16_close
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 V2 = [int(ln.split()[0]) for ln in nat.list_variants() if ln.split()[1].startswith("v2")]
-QS = [QParams(16, b, g, s) for b in (4, 8) for g in (-1, 128) for s in (True, False)]
+QS = [QParams(16, b, g, s) for b in (2, 4, 8) for g in (-1, 128) for s in (True, False)]
 
 
 def _check(hps):
@@ -31,7 +31,7 @@ def test_weightonly_edge_shapes(q, variant):
     _check(hps)
 
 
-@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("bits", [2, 4, 8])
 def test_reference_format_weights_through_repack(bits):
     """B built in the reference's packed format (permute_weight + pack_weightonly), converted by
     mxmoe_gg_repack_weightonly, then run — the drop-in route for reference-packed weights."""
@@ -46,10 +46,10 @@ def test_reference_format_weights_through_repack(bits):
 def test_all_quant_types_in_one_launch(variant):
     specs = [(300, 256, 256, W8A8), (129, 384, 512, W4A4), (77, 128, 192, FP16), (260, 256, 1408, QParams(16, 4, 128, False)),
              (33, 512, 2048, QParams(16, 8, -1, True)), (0, 256, 256, QParams(16, 4, -1, True)),
-             (513, 264, 640, QParams(16, 4, 64, True))]
+             (513, 264, 640, QParams(16, 4, 64, True)), (96, 256, 512, QParams(16, 2, 128, False))]
     hps = [HostProblem(M, N, K, q, seed=70 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)
-    assert gg.info.qtype_mask == 0b11111
+    assert gg.info.qtype_mask == 0b1011111
     gg.launch()
     torch.cuda.synchronize()
     _check(hps)
