@@ -81,6 +81,9 @@ def main(argv=None):
     ap.add_argument("--variants", type=str, default=None, help="comma list (default: tile_config or all)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-baseline", action="store_true")
+    ap.add_argument("--cpu-plumbing", action="store_true",
+                    help="no GPU: write the workload JSON and time the per-problem torch.matmul fp16 baseline on "
+                         "the host (BASELINE configs[0]: bs=128 plumbing); the HIP kernels are not run")
     args = ap.parse_args(argv)
 
     suffix, wl_kw, qcfg_list = workload_suffix(args)
@@ -97,6 +100,8 @@ def main(argv=None):
     from mxmoe_amd.groupgemm import GroupGemm
     from mxmoe_amd.tile_config import parse_tile_config_json, select_variant
 
+    if args.cpu_plumbing:
+        return cpu_plumbing(args, trace, layers, wl_kw, workload_path, suffix)
     nat.lib()  # fails loudly if the HIP library is missing
     for layer in layers:
         print(f"Processing Layer {layer}...")
@@ -149,6 +154,43 @@ def main(argv=None):
             del inp
             torch.cuda.empty_cache()
         print(f"Layer {layer} completed! Results saved to: {bench_save}")
+
+
+def cpu_plumbing(args, trace, layers, wl_kw, workload_path, suffix):
+    """BASELINE configs[0]: the workload plumbing plus the reference's torch CPU matmul path (fp16,
+    one torch.matmul per problem) timed on the host. Nothing here runs or stands in for the HIP
+    kernels; it is the baseline the GPU numbers are reported against."""
+    import time
+
+    import torch
+
+    from mxmoe_amd.harness import write_csv
+
+    out = []
+    for layer in layers:
+        wl = generate_workload_from_trace(trace, args.bs, layer, **wl_kw)
+        save_workload(wl, workload_path)
+        print(f"Save generated workloads to `{workload_path}`")
+        parsed = load_workload(wl)[f"layer-{layer}"]
+        g = torch.Generator().manual_seed(42)
+        for gg in ("gate_up", "down"):
+            fp = [((torch.rand(max(s.M, 1), s.K, generator=g) * 2 - 1).half(),
+                   (torch.rand(s.N, s.K, generator=g) * 2 - 1).half()) for s in parsed[gg]]
+            flops = sum(2.0 * s.M * s.N * s.K for s in parsed[gg])
+            for a, b in fp[:2]:
+                torch.matmul(a, b.t())  # warm-up
+            t0 = time.perf_counter()
+            for a, b in fp:
+                torch.matmul(a, b.t())
+            ms = (time.perf_counter() - t0) * 1e3
+            row = {"kernel_name": "torch.matmul_fp16_per_problem_cpu", "avg_time": ms,
+                   "TFLOPS": flops / (ms * 1e-3) / 1e12, "speedup": 1.0}
+            bench_save = f"{CUR_DIR}/out/bench/{args.model}-{args.dataset}-{args.bs}{suffix.replace('.json', '')}"
+            write_csv(f"{bench_save}-layer-{layer}-{gg}-cpu.csv", [row])
+            print(f"  {gg} cpu torch.matmul fp16: {ms:.2f} ms  {row['TFLOPS'] * 1e3:.2f} GFLOP/s "
+                  f"({len(parsed[gg])} problems, {torch.get_num_threads()} threads)")
+            out.append((layer, gg, len(parsed[gg]), ms))
+    return out
 
 
 if __name__ == "__main__":

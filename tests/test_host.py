@@ -136,3 +136,24 @@ def test_ds2_mixed_allocation_pinned():
     layer = wl.load_workload(wl.ds2_workload(8192, qconfig=wl.ds2_mixed_qconfig()))["layer-1"]
     assert sum(p.M for p in layer["gate_up"][:-1]) == 8192 * 6 and layer["gate_up"][-1].shape == [8192, 5632, 2048]
     assert layer["down"][-1].shape == [8192, 2048, 2816]
+
+
+def test_cpu_plumbing_bs128_config0(tmp_path, monkeypatch):
+    """BASELINE configs[0]: `run_mxmoe_gg.py --bs 128 --cpu-plumbing` writes the layer-11 workload
+    (61 problems per GroupGEMM, shared expert last with M = 128, routed M_e = int(p_e * 128 * 4)) and
+    times the per-problem torch.matmul fp16 path on the host — no GPU, no HIP kernel."""
+    import json
+
+    import run_mxmoe_gg as cli
+    from mxmoe_amd.workload import qwen2_hist
+
+    monkeypatch.setattr(cli, "CUR_DIR", str(tmp_path))
+    out = cli.main(["--model", "qwen2_moe", "--bs", "128", "--layer", "11", "--cpu-plumbing"])
+    assert [(gg, n) for _, gg, n, _ in out] == [("gate_up", 61), ("down", 61)]
+    wl = json.load(open(tmp_path / "out" / "workloads" / "qwen2_moe-wiki2-128-fp16.json"))
+    gate_up = wl["layer-11"]["gate_up"]
+    assert gate_up[-1]["shape"] == [128, 11264, 2048]
+    h = qwen2_hist()["M"]
+    tot = sum(h)
+    assert [p["shape"][0] for p in gate_up[:-1]] == [int(m / tot * 128 * 4) for m in h]
+    assert (tmp_path / "out" / "bench" / "qwen2_moe-wiki2-128-fp16-layer-11-gate_up-cpu.csv").exists()
