@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from mxmoe_amd import _native as nat
-from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, GroupGemm, QParams, group_gemm, groupgemm_reference_abi
+from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, GroupGemm, Problem, QParams, group_gemm, groupgemm_reference_abi
 from tests._util import HostProblem, assert_f16_close
 
 pytestmark = pytest.mark.gpu
@@ -189,3 +189,39 @@ def test_splitk_long_k_low_fill(q, variant):
     torch.cuda.synchronize()
     for h, c in zip(hps, first):
         assert torch.equal(h.problem.C.view(torch.int16), c.view(torch.int16))
+
+
+@pytest.mark.parametrize("q", [FP16, W8A8], ids=["fp16", "w8a8"])
+def test_64bit_offsets_large_c(q):
+    """C of 65536 x 33024 (2.16e9 elements > 2^31): row offsets into C (and A) need 64-bit address
+    arithmetic in the DMA sources and the epilogue stores. Checked on the last rows and columns
+    against a torch fp32 reference of the same op (fp16: within tolerance; w8a8: bit-exact, the
+    reference epilogue fp16(f32(acc) * f32(fp16(sa * sb))) with |acc| < 2^24). The pack_wxax byte
+    order is the same permutation on A and B, so raw int8 rows stand in for packed ones."""
+    M, N, K = 65536, 33024, 128
+    g = torch.Generator(device=DEV).manual_seed(5)
+    if q.is_quant:
+        A = torch.randint(-127, 128, (M, K), generator=g, device=DEV, dtype=torch.int8).view(torch.uint8)
+        B = torch.randint(-127, 128, (N, K), generator=g, device=DEV, dtype=torch.int8).view(torch.uint8)
+        sa = (torch.rand(M, generator=g, device=DEV) * 1e-3 + 1e-4).half()
+        sb = (torch.rand(N, generator=g, device=DEV) * 1e-3 + 1e-4).half()
+    else:
+        A = (torch.rand(M, K, generator=g, device=DEV) * 2 - 1).half()
+        B = (torch.rand(N, K, generator=g, device=DEV) * 2 - 1).half()
+        sa = sb = None
+    C = torch.empty(M, N, dtype=torch.float16, device=DEV)
+    group_gemm([Problem(A=A, B=B, C=C, M=M, N=N, K=K, q=q, scale_a=sa, scale_b=sb)])
+    torch.cuda.synchronize()
+    rows = torch.tensor([0, 1, 32767, 32768, 50000, 65534, 65535], device=DEV)
+    cols = torch.cat([torch.arange(0, 64, device=DEV), torch.arange(N - 64, N, device=DEV)])
+    got = C[rows][:, cols].float()
+    if q.is_quant:
+        acc = A[rows].view(torch.int8).float() @ B[cols].view(torch.int8).float().t()  # exact: |acc| < 2^24
+        s = (sa[rows][:, None] * sb[cols][None, :]).float()  # fp16 products, correctly rounded
+        ref = (acc * s).half().float()
+        assert torch.equal(got, ref)
+    else:
+        ref = A[rows].float() @ B[cols].float().t()
+        assert torch.allclose(got, ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
+    del C
+    torch.cuda.empty_cache()
