@@ -140,6 +140,8 @@ struct ActArgs {
   int nseg;
   uint8_t* out;
   _Float16* scales;
+  int64_t blk_shared;          // parts > 1: first workgroup of the shared rows (one row per workgroup)
+  int parts;                   // 1, or 4: a shared row is split over the 4 waves of its workgroup
 };
 
 // quant_weight arithmetic (quantize.cuh:218-279): scale = fp16(amax / qmax), 0 -> 1;
@@ -203,12 +205,18 @@ __device__ __forceinline__ float amax8(const h8_t& x) {
 // One WAVE per slot row (4 rows per 256-thread workgroup): lane l holds elements c*512 + 8l .. +7
 // of chunk c in registers (MAXC chunks: rows up to MAXC*512 elements), so every lane has MAXC
 // independent 16-B loads in flight, the per-token amax is a wave butterfly and a 128-element group
-// is 16 adjacent lanes — no LDS, no barrier.
+// is 16 adjacent lanes — no LDS, no barrier. parts == 4: the workgroups from blk_shared on take one
+// wide shared row each, wave w its w-th run of 128-aligned columns (the per-token amax then crosses
+// the 4 waves through LDS), so routed and shared rows share one launch and one register budget.
 template <bool SILU, int MAXC>
 __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
+  __shared__ float wave_amax[kThreads / 64];
   const int lane = threadIdx.x & 63;
-  const int64_t s = a.s0 + (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (s >= a.nslots) return;
+  const bool split_row = a.parts > 1 && (int64_t)blockIdx.x >= a.blk_shared;  // workgroup-uniform
+  const int part = split_row ? (int)(threadIdx.x >> 6) : 0;
+  const int64_t s = split_row ? a.ntk + ((int64_t)blockIdx.x - a.blk_shared)
+                              : a.s0 + (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  if (s >= (a.parts > 1 && !split_row ? a.ntk : a.nslots)) return;  // split_row: uniform
   int e;
   const _Float16* row_src;
   if (s < a.ntk) {
@@ -223,8 +231,12 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const mxmoe_moe_seg sg = a.segs[e];
   const int64_t row = s - sg.first_slot;
   if (row < 0 || row >= sg.rows) return;  // slot outside its segment (inconsistent table): never write
-  const int width = sg.width;
   const int upoff = SILU ? (s < a.ntk ? a.N : a.Ns) : 0;  // column of the "up" half
+  // this wave's columns [col0, col0 + width) of the row (split rows: 128-aligned quarter runs)
+  const int qw = split_row ? ((sg.width / 4 + 127) & ~127) : sg.width;
+  const int col0 = part * qw;
+  const int width = split_row ? max(0, min(qw, sg.width - col0)) : sg.width;
+  row_src += col0;
 
   // every load of the row first (all in flight together), then the arithmetic
   h8_t x[MAXC];
@@ -241,7 +253,8 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   }
   if constexpr (SILU) {
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int c = 0; c < MAXC; ++c) {
+      if (c * 512 < width)  // uniform: chunks past the row stay zero (silu(0) * 0 = 0)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         // silu(g) = g / (1 + e^-g) with the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: the
@@ -250,10 +263,11 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
         const float sg = g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(g * -1.4426950408889634f));
         x[c][j] = (_Float16)(sg * (float)u[c][j]);
       }
+    }
   }
 
   if (sg.qtag == MXMOE_ACT_FP16) {
-    _Float16* o = reinterpret_cast<_Float16*>(a.out + sg.out_off) + row * width;
+    _Float16* o = reinterpret_cast<_Float16*>(a.out + sg.out_off) + row * sg.width + col0;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int idx = c * 512 + lane * 8;
@@ -264,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const int bits = sg.qtag == MXMOE_ACT_INT8 ? 8 : 4;
   const float qmax = bits == 8 ? 127.0f : 7.0f;
   const h2_t lim = {(_Float16)qmax, (_Float16)qmax};
-  uint8_t* o = a.out + sg.out_off + row * (int64_t)width * bits / 8;
+  uint8_t* o = a.out + sg.out_off + (row * (int64_t)sg.width + col0) * bits / 8;
   if (sg.qtag == MXMOE_ACT_INT4_G128) {
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -277,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
         const _Float16 sc = rtn_scale(m, qmax);
         const float rs = __builtin_amdgcn_rcpf((float)sc);
         *reinterpret_cast<uint32_t*>(o + idx / 2) = codes_i4(x[c], (float)sc, rs, lim);
-        if ((lane & 15) == 0) a.scales[sg.scale_off + (int64_t)(idx / 128) * sg.rows + row] = sc;
+        if ((lane & 15) == 0) a.scales[sg.scale_off + (int64_t)((col0 + idx) / 128) * sg.rows + row] = sc;
       }
     }
     return;
@@ -287,9 +301,14 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   for (int c = 0; c < MAXC; ++c) m = fmaxf(m, amax8(x[c]));  // chunks past the row are zeros
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  if (split_row) {  // every wave of the workgroup reaches here (its row's checks are uniform)
+    if (lane == 0) wave_amax[part] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(wave_amax[0], wave_amax[1]), fmaxf(wave_amax[2], wave_amax[3]));
+  }
   const _Float16 sc = rtn_scale(m, qmax);
   const float rs = __builtin_amdgcn_rcpf((float)sc);
-  if (lane == 0) a.scales[sg.scale_off + row] = sc;
+  if (lane == 0 && part == 0) a.scales[sg.scale_off + row] = sc;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int idx = c * 512 + lane * 8;
@@ -337,17 +356,34 @@ using namespace mxmoe;
 
 template <bool SILU>
 static void launch_act_w(const ActArgs& a, int maxw, hipStream_t st) {
-  const dim3 grid((unsigned)((a.nslots - a.s0 + kThreads / 64 - 1) / (kThreads / 64))), block(kThreads);
+  const int64_t blocks = a.parts > 1 ? a.blk_shared + (a.nslots - a.ntk)
+                                     : (a.nslots - a.s0 + kThreads / 64 - 1) / (kThreads / 64);
+  const dim3 grid((unsigned)blocks), block(kThreads);
   if (maxw <= 2048) hipLaunchKernelGGL((act_quant_kernel<SILU, 4>), grid, block, 0, st, a);
   else if (maxw <= 4096) hipLaunchKernelGGL((act_quant_kernel<SILU, 8>), grid, block, 0, st, a);
   else if (maxw <= 8192) hipLaunchKernelGGL((act_quant_kernel<SILU, 16>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((act_quant_kernel<SILU, 32>), grid, block, 0, st, a);
 }
 
-// slots [0, nslots): one launch, or (rows of different widths) routed slots [0, ntk) and shared
-// slots [ntk, nslots) as two launches, each with the register row of its own width
+// slots [0, nslots): one launch; rows of different widths (routed [0, ntk), shared [ntk, nslots)):
+// one launch with each shared row split over a workgroup's 4 waves when a quarter of the shared row
+// fits the routed rows' register width, else two launches, each with the register row of its width
 static int launch_act(bool silu, ActArgs a, int64_t nslots, int w_routed, int w_shared, void* stream) {
   if (nslots == 0) return MXMOE_GG_OK;
+  a.parts = 1;
+  a.blk_shared = 0;
+  const int qw = (w_shared / 4 + 127) & ~127;
+  if (nslots > a.ntk && a.ntk > 0 && w_shared > w_routed && qw <= w_routed) {
+    a.parts = 4;
+    a.blk_shared = (a.ntk + kThreads / 64 - 1) / (kThreads / 64);
+    a.s0 = 0;
+    a.nslots = nslots;
+    if (silu) launch_act_w<true>(a, w_routed, (hipStream_t)stream);
+    else launch_act_w<false>(a, w_routed, (hipStream_t)stream);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "act_quant_kernel launch failed: %s", hipGetErrorString(e));
+    return MXMOE_GG_OK;
+  }
   const bool split = nslots > a.ntk && w_routed != w_shared && a.ntk > 0;
   a.s0 = 0;
   a.nslots = split ? a.ntk : nslots;

@@ -130,15 +130,17 @@ def test_gg_permute_inp_mirror(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,Ns", [(256, 512), (1408, 5632)])
-def test_silu_mul_quant_within_one_step(gpu, N, Ns):
+# (256, 640): the shared row's quarter runs are 256, 256, 128 and 0 columns (one launch, split rows)
+@pytest.mark.parametrize("N,Ns", [(256, 512), (1408, 5632), (256, 640), (512, 512)])
+@pytest.mark.parametrize("shared_tag", [0, 1, 2, 3])
+def test_silu_mul_quant_within_one_step(gpu, N, Ns, shared_tag):
     T, topk, E = 61, 4, 8
     ids = _ids(T, topk, E, 7)
     r = moe.route(ids.to(DEV), E)
     g = torch.Generator().manual_seed(8)
     routed = ((torch.rand(T * topk, 2 * N, generator=g) * 2 - 1) * 4).half()
     shared = ((torch.rand(T, 2 * Ns, generator=g) * 2 - 1) * 4).half()
-    tags = [0, 1, 2, 3, 0, 1, 2, 3, 0]
+    tags = [0, 1, 2, 3, 0, 1, 2, 3, shared_tag]
     b = moe.silu_mul_quant(routed.to(DEV), shared.to(DEV), r, tags)
     torch.cuda.synchronize()
     act_r = moe_ref.silu_mul(routed.numpy())
