@@ -95,7 +95,7 @@ def strong_scaling_rccl(cfg: str, dev, world: int, rank: int, steps: int = 10, w
 
     from mxmoe_amd.dist import nslice_plan, shard_bytes
     from mxmoe_amd.groupgemm import GroupGemm
-    from mxmoe_amd.harness import build_layer_inputs
+    from mxmoe_amd.harness import build_layer_inputs, slice_scale_b
 
     def timed(fn):
         for _ in range(warmup):
@@ -126,7 +126,7 @@ def strong_scaling_rccl(cfg: str, dev, world: int, rank: int, steps: int = 10, w
             n = p.M * w.width
             mine.append(dataclasses.replace(p, B=p.B[w.n0:w.n1], N=w.width, ldc=0,
                                             C=local[off:off + n].view(max(p.M, 1), w.width),
-                                            scale_b=None if p.scale_b is None else p.scale_b[w.n0:w.n1]))
+                                            scale_b=slice_scale_b(p, w.n0, w.n1)))
             off += n
         part = GroupGemm(mine, device=dev) if mine else None
 

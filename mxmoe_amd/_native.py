@@ -176,6 +176,17 @@ def list_variants() -> list[str]:
     return [ln for ln in buf.value.decode().splitlines() if ln]
 
 
+def variant_supports(variant: int, qcfg: str) -> bool:
+    """Whether a compiled variant has a tile body for ``qcfg`` (weight-only strategies are listed by
+    their base name, e.g. ``w4a16``)."""
+    from .tile_config import variant_key
+
+    if variant == VARIANT_AUTO:
+        return True
+    line = list_variants()[variant]
+    return f" {variant_key(qcfg)}=TileConfig(" in line
+
+
 def variant_tile(variant: int, a_bits: int, w_bits: int) -> dict:
     v = [ctypes.c_int32() for _ in range(4)]
     check(lib().mxmoe_gg_variant_tile(variant, a_bits, w_bits, *[ctypes.byref(x) for x in v]))

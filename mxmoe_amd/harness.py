@@ -111,11 +111,24 @@ def write_csv(path: str, rows: list[dict]) -> None:
             w.writerow([r["kernel_name"], f"{r['avg_time']:.6f}", f"{r['TFLOPS']:.3f}", f"{r['speedup']:.3f}"])
 
 
+def slice_scale_b(p: Problem, n0: int, n1: int) -> Optional[torch.Tensor]:
+    """scale_b entries of columns [n0, n1) in the layout the kernel reads for an N' = n1 - n0 problem:
+    per-channel [N] -> a view; grouped [G][N] (w4a4 g128, weight-only sym) and weight-only asym
+    [G][N][2] -> a contiguous copy of the [:, n0:n1] block (the kernel reads G x N' entries)."""
+    if p.scale_b is None:
+        return None
+    q = p.q
+    G = 1 if q.gsize == -1 else p.K // q.gsize
+    if G == 1 and not (q.is_weight_only and not q.sym):
+        return p.scale_b[n0:n1]
+    return p.scale_b.reshape(G, p.N, -1)[:, n0:n1].contiguous().reshape(-1)
+
+
 def slice_problem(p: Problem, n0: int, n1: int) -> Problem:
-    """Columns [n0, n1) of a problem as a strided view: B rows / scale_b entries n0..n1 (contiguous),
-    C columns n0..n1 (row stride = the full problem's ldc). No copy."""
+    """Columns [n0, n1) of a problem: B rows n0..n1 (a view), C columns n0..n1 (strided view, row
+    stride = the full problem's ldc), scale_b per slice_scale_b (a copy only for grouped layouts)."""
     return dataclasses.replace(p, B=p.B[n0:n1], C=p.C[:, n0:n1], N=n1 - n0, ldc=p.ldc or p.N,
-                               scale_b=None if p.scale_b is None else p.scale_b[n0:n1])
+                               scale_b=slice_scale_b(p, n0, n1))
 
 
 def strong_scaling_sim(inputs: LayerInputs, worlds: Sequence[int] = (2, 4, 8), warmup: int = 5,

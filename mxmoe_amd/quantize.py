@@ -143,3 +143,43 @@ def pack_weightonly_mi355x(codes: torch.Tensor, bits: int) -> torch.Tensor:
         return u.reshape(N, K).contiguous()
     u = u[..., [0, 2, 4, 6, 1, 3, 5, 7]].reshape(N, K)
     return (u[:, 0::2] | (u[:, 1::2] << 4)).contiguous()
+
+
+def unpack_weightonly_mi355x(packed: torch.Tensor, bits: int, K: int) -> torch.Tensor:
+    """Inverse of pack_weightonly_mi355x: kernel layout uint8 [N, K * bits / 8] -> stored codes uint8 [N, K]."""
+    N = packed.shape[0]
+    if K % 64:
+        raise ValueError("weight-only needs K % 64 == 0")
+    if bits == 2:
+        word = packed.contiguous().view(torch.int32).reshape(N, K // 64, 4).to(torch.int64)
+        e = torch.arange(8)
+        shift = (((e % 2) * 16)[None, :] + 2 * (4 * torch.arange(2)[:, None] + e[None, :] // 2)).to(packed.device)
+        u = (word[..., None, None] >> shift) & 3  # [N, seg, g, kc, e]
+        return u.transpose(2, 3).reshape(N, K).to(torch.uint8)
+    if bits == 8:
+        return packed.reshape(N, K // 64, 4, 2, 8).transpose(2, 3).reshape(N, K).contiguous()
+    if bits != 4:
+        raise ValueError("weight-only: 2 / 4 / 8-bit codes")
+    lo, hi = packed & 0xF, packed >> 4
+    u = torch.stack([lo, hi], dim=-1).reshape(N, K // 64, 4, 2, 8)  # [N, seg, g, kc, stored position]
+    inv = torch.tensor([0, 4, 1, 5, 2, 6, 3, 7], device=packed.device)  # position p holds e = [0,2,4,6,1,3,5,7][p]
+    u = u.index_select(-1, inv)
+    return u.transpose(2, 3).reshape(N, K).contiguous()
+
+
+def dequant_weightonly(codes: torch.Tensor, sz: torch.Tensor, bits: int, gsize: int, sym: bool) -> torch.Tensor:
+    """Stored codes uint8 [N, K] + kernel-layout scale_zp ([G][N] sym, [G][N][2] asym) -> the fp16 B the
+    kernels multiply: fp16(fma(u - off, scale, zp)), one rounding (Converter::dequant_frag,
+    quantize.cuh:146-213; off = 2^(bits-1) - 1 for sym codes, pack_weightonly quantize.cuh:387-421)."""
+    N, K = codes.shape
+    G = 1 if gsize == -1 else K // gsize
+    g = K if gsize == -1 else gsize
+    if sym:
+        s = sz.reshape(G, N).t().double()
+        z = torch.zeros_like(s)
+    else:
+        t = sz.reshape(G, N, 2).transpose(0, 1).double()
+        s, z = t[..., 0], t[..., 1]
+    off = (1 << (bits - 1)) - 1 if sym else 0
+    u = codes.to(torch.float64).reshape(N, G, g) - off
+    return (u * s[..., None] + z[..., None]).reshape(N, K).half()  # exact in f64, then one rounding

@@ -135,20 +135,34 @@ def mi355x_variants() -> list[dict]:
     return out
 
 
-def select_variant(tile_cfgs: Optional[dict] = None, default: int = 0) -> int:
-    """Nearest compiled variant to the requested per-qcfg tiles (log-area + aspect distance)."""
+def variant_key(qcfg: str) -> str:
+    """The key a variant lists a qcfg under: weight-only strategies by their base name
+    (``w4a16_g128_asym`` -> ``w4a16``: one tile body serves every group size / symmetry);
+    wxax and fp16 strategies by their full name (``w4a4_g128_sym`` is its own body)."""
+    m = re.match(r"^(w\d+a16)_g-?\d+_a?sym$", qcfg)
+    return m.group(1) if m else qcfg
+
+
+def select_variant(tile_cfgs: Optional[dict] = None, default: int = 0, variants: Optional[list] = None) -> int:
+    """Nearest compiled variant to the requested per-qcfg tiles (log-area + aspect distance).
+
+    A variant with no tile body for one of the requested qcfgs is never chosen (infinite distance);
+    if no variant covers all of them, ``default`` is returned."""
     if not tile_cfgs:
         return default
     import math
 
     best, best_d = default, float("inf")
-    for v in mi355x_variants():
+    for v in (mi355x_variants() if variants is None else variants):
         d = 0.0
         for q, lst in tile_cfgs.items():
-            if q not in v["tiles"] or not lst:
-                continue
-            want, have = lst[0], v["tiles"][q]
-            d += abs(math.log2(want.BM / have.BM)) + abs(math.log2(want.BN / have.BN))
+            have = v["tiles"].get(variant_key(q))
+            if have is None:
+                d = float("inf")
+                break
+            if lst:
+                want = lst[0]
+                d += abs(math.log2(want.BM / have.BM)) + abs(math.log2(want.BN / have.BN))
         if d < best_d:
             best, best_d = v["id"], d
     log.warning("tile_config mapped to MI355X variant %d (reference tiles are sm80/sm89 CUDA tiles)", best)

@@ -103,6 +103,7 @@ def main(argv=None):
     if args.cpu_plumbing:
         return cpu_plumbing(args, trace, layers, wl_kw, workload_path, suffix)
     nat.lib()  # fails loudly if the HIP library is missing
+    result = {"qcfg_list": qcfg_list, "variants": {}, "csv": []}
     for layer in layers:
         print(f"Processing Layer {layer}...")
         wl = generate_workload_from_trace(trace, args.bs, layer, **wl_kw)
@@ -118,9 +119,10 @@ def main(argv=None):
         elif args.tile_config:
             tiles = parse_tile_config_json(args.tile_config, qcfg_list, layer)
             variants = [select_variant(tiles, nat.default_variant())]
-        else:
-            variants = nat.production_variants()
+        else:  # every compiled variant that has a tile body for each qcfg of the layer
+            variants = [v for v in nat.production_variants() if all(nat.variant_supports(v, q) for q in qcfg_list)]
         names = nat.list_variants()
+        result["variants"][layer] = variants
         parsed = load_workload(wl)[f"layer-{layer}"]
         for gg in ("gate_up", "down"):
             inp = build_layer_inputs(parsed[gg])
@@ -151,9 +153,11 @@ def main(argv=None):
                 print(f"  {gg} {names[v].split()[1]}: {t['median_ms']:.4f} ms  {tf:.1f} TFLOP/s")
             bench_save = f"{CUR_DIR}/out/bench/{args.model}-{args.dataset}-{args.bs}{suffix.replace('.json', '')}"
             write_csv(f"{bench_save}-layer-{layer}-{gg}.csv", rows)
+            result["csv"].append(f"{bench_save}-layer-{layer}-{gg}.csv")
             del inp
             torch.cuda.empty_cache()
         print(f"Layer {layer} completed! Results saved to: {bench_save}")
+    return result
 
 
 def cpu_plumbing(args, trace, layers, wl_kw, workload_path, suffix):

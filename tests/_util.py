@@ -86,3 +86,26 @@ def assert_f16_close(out: np.ndarray, ref: np.ndarray, K: int):
     bad = np.abs(out - ref) > tol
     assert not bad.any(), f"{bad.sum()} / {bad.size} fp16 outputs outside tolerance; max err " \
                           f"{np.max(np.abs(out - ref))}"
+
+
+def assert_fakequant_close(out: np.ndarray, ref_fq: np.ndarray, what: str = ""):
+    """Parity against the reference's executed definition of a quantised linear,
+    C_fq = F.linear(Quantizer.fake_quant(a), Quantizer.fake_quant(b)) in fp32 (quant.py:87-106).
+
+    The two computations are equal in exact arithmetic; they round differently: fake_quant rounds
+    every dequantised operand q*s (+zp) to fp16 (relative 2^-11 each) and sums in fp32, the kernel
+    path forms the exact integer dot product, rounds sa*sb to fp16 and the output to fp16. Bar:
+      norm-wise  ||out - C_fq|| <= 1e-3 ||C_fq||            (north_star's 1e-3 relative)
+      elementwise |out - C_fq| <= 1e-3 |C_fq| + 4e-3 rms(C_fq)   (cancellation floor)
+    Measured on the fixtures: norm-wise 2-5e-4, elementwise excess <= 1.9e-3 rms."""
+    out = out.astype(np.float64)
+    ref = ref_fq.astype(np.float64)
+    assert out.shape == ref.shape, (out.shape, ref.shape)
+    if ref.size == 0:
+        return
+    assert np.isfinite(out).all(), f"{what}: non-finite output"
+    nref = float(np.linalg.norm(ref))
+    assert float(np.linalg.norm(out - ref)) <= 1e-3 * nref, f"{what}: norm-wise error above 1e-3"
+    rms = nref / np.sqrt(ref.size)
+    bad = np.abs(out - ref) > 1e-3 * np.abs(ref) + 4e-3 * rms
+    assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} outputs outside the fake-quant tolerance"

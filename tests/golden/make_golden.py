@@ -21,7 +21,14 @@ writes into the source tree, compose_kernel.py:556), with two shims that change 
                            plus the reference-as-written column-scale permutation (mm_tile.cuh:452,462)
 The LP-derived mixed qconfig is solved exactly (0/1 knapsack DP) from bits_model-1.lp.
 
-Usage: python tests/golden/make_golden.py [--only-g128]
+  gg_fakequant_ref.npz ... the reference's OWN definition of a quantised linear, executed: for every
+                           problem of the gg_*_small vectors, C_fq = F.linear(Quantizer.fake_quant(a),
+                           Quantizer.fake_quant(b)) in fp32 (quant.py:87-106); plus weight-only
+                           vectors (w2/w4/w8 a16, g-1 / g128, sym / asym): fp16 A, B, the reference's
+                           quant_minmax codes / scales / zero points of B and
+                           C_fq = F.linear(A, Quantizer(bits, sym, gsize).fake_quant(B))
+
+Usage: python tests/golden/make_golden.py [--only-g128 | --only-fq]
 """
 from __future__ import annotations
 
@@ -63,8 +70,8 @@ def import_reference():
     sys.path.insert(0, str(TMP))
     import run_mxmoe_gg  # noqa: F401
     from mxmoe.kernels import compose_kernel, gen_workload, tile_config
-    from mxmoe.quant.quant import quant_minmax
-    return types.SimpleNamespace(quant_minmax=quant_minmax, get_qcfg_list=run_mxmoe_gg.get_qcfg_list,
+    from mxmoe.quant.quant import Quantizer, quant_minmax
+    return types.SimpleNamespace(quant_minmax=quant_minmax, Quantizer=Quantizer, get_qcfg_list=run_mxmoe_gg.get_qcfg_list,
                                  compose_kernel=compose_kernel, tile_config=tile_config, gen_workload=gen_workload)
 
 
@@ -253,11 +260,68 @@ def make_g128(ref):
     np.savez_compressed(HERE / "gg_w4a4g128_small.npz", **make_g128_vectors(ref, specs, seed=128))
 
 
+# ------------------------------------------------------------------ reference-executed fake-quant C
+
+FQ_SOURCES = {  # fixture -> (seed, specs) exactly as main() / make_g128() build them
+    "w8a8": ("gg_w8a8_small.npz", 42), "w4a4": ("gg_w4a4_small.npz", 43), "mixed": ("gg_mixed_small.npz", 45),
+    "w4a4g128": ("gg_w4a4g128_small.npz", 128)}
+
+WO_SPECS = [  # (M, N, K, w_bits, gsize, sym): weight-only problems, A fp16
+    (17, 128, 256, 4, -1, True), (130, 256, 384, 4, -1, False), (33, 128, 512, 4, 128, False),
+    (64, 256, 256, 4, 128, True), (77, 128, 256, 8, -1, False), (9, 128, 384, 8, 128, False),
+    (40, 256, 256, 8, -1, True), (21, 128, 512, 2, 128, False), (50, 128, 256, 2, -1, False),
+    (1, 128, 1024, 4, 128, False)]
+
+
+def make_fakequant(ref):
+    """gg_fakequant_ref.npz: the reference's Quantizer.fake_quant (quant.py:87-106) run on the same
+    seeded fp16 inputs as the committed GroupGEMM vectors, then F.linear in fp32. The codes of each
+    regenerated input are first checked against the committed fixture (same seed stream)."""
+    import torch.nn.functional as F
+
+    out = {}
+    for kind, (fname, seed) in FQ_SOURCES.items():
+        d = np.load(HERE / fname)
+        g = torch.Generator().manual_seed(seed)
+        for i in range(int(d["P"])):
+            M, N, K = (int(x) for x in d[f"p{i}_shape"])
+            a = (torch.rand(M, K, generator=g) * 2 - 1).half()
+            b = (torch.rand(N, K, generator=g) * 2 - 1).half()
+            bits = int(d[f"p{i}_bits"])
+            if bits == 16:
+                continue
+            gsize = 128 if kind == "w4a4g128" else -1
+            qa, _, _ = ref.quant_minmax(a, bits, gsize, True)
+            qb, _, _ = ref.quant_minmax(b, bits, gsize, True)
+            assert (qa.to(torch.int8).numpy() == d[f"p{i}_qa"]).all() and (qb.to(torch.int8).numpy() == d[f"p{i}_qb"]).all()
+            qz = ref.Quantizer(bits, True, gsize)
+            cfq = F.linear(qz.fake_quant(a).float(), qz.fake_quant(b).float()) if M else torch.zeros(0, N)
+            out[f"{kind}_p{i}_Cfq"] = cfq.numpy().astype(np.float32)
+    g = torch.Generator().manual_seed(777)
+    out["wo_P"] = np.int32(len(WO_SPECS))
+    for i, (M, N, K, bits, gsize, sym) in enumerate(WO_SPECS):
+        a = (torch.rand(M, K, generator=g) * 2 - 1).half()
+        b = (torch.rand(N, K, generator=g) * 2 - 1).half()
+        q, s, z = ref.quant_minmax(b, bits, gsize, sym)
+        qz = ref.Quantizer(bits, sym, gsize)
+        out[f"wo{i}_spec"] = np.array([M, N, K, bits, gsize, int(sym)], np.int32)
+        out[f"wo{i}_A"], out[f"wo{i}_B"] = a.numpy(), b.numpy()
+        out[f"wo{i}_q"] = q.to(torch.uint8 if not sym else torch.int8).numpy()
+        G = 1 if gsize == -1 else K // gsize
+        out[f"wo{i}_scale"] = s.reshape(N, G).numpy().astype(np.float16)
+        out[f"wo{i}_zp"] = (np.zeros((N, G), np.float16) if sym else z.reshape(N, G).numpy().astype(np.float16))
+        out[f"wo{i}_Cfq"] = F.linear(a.float(), qz.fake_quant(b).float()).numpy().astype(np.float32)
+    np.savez_compressed(HERE / "gg_fakequant_ref.npz", **out)
+
+
 def main():
     sys.path.insert(0, str(ROOT))
     ref = import_reference()
     if "--only-g128" in sys.argv:
         make_g128(ref)
+        return
+    if "--only-fq" in sys.argv:
+        make_fakequant(ref)
         return
     torch.manual_seed(0)
 
@@ -350,6 +414,7 @@ def main():
              (33, 256, 128, "fp16"), (257, 128, 256, "w8a8_g-1_sym"), (9, 256, 1024, "w4a4_g-1_sym")]
     np.savez_compressed(HERE / "gg_mixed_small.npz", **make_gg_vectors(ref, "mixed", mixed, 45))
     make_g128(ref)
+    make_fakequant(ref)
     print("golden fixtures written;", meta)
 
 
