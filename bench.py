@@ -152,41 +152,84 @@ def strong_scaling_rccl(cfg: str, dev, world: int, rank: int, steps: int = 10, w
     return out
 
 
-def cpu_baseline(cfg: str, shapes, budget_s: float = 15.0) -> dict:
-    """The CPU oracle (port of the reference arithmetic) timed on this host's cores, bounded sample."""
-    import numpy as np
+def cpu_info() -> dict:
+    """Host CPU model and the threads the baseline may use (the GPU box exports OMP_NUM_THREADS=16:
+    its share of a much larger machine, which os.cpu_count() would report)."""
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)))
+    return {"model": model, "threads": max(1, threads), "visible_cpus": avail}
 
-    from oracle import oracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))
-    rng = np.random.default_rng(0)
-    done_flops, t_used, names = 0, 0.0, []
-    probs = [(gg, s) for gg in ("gate_up", "down") for s in shapes[gg][:-1]]
-    for gg, s in probs:
-        M, N, K = s.M, s.N, s.K
-        if s.qcfg == "fp16":
-            A = (rng.random((M, K), np.float32) * 2 - 1).astype(np.float16)
-            B = (rng.random((N, K), np.float32) * 2 - 1).astype(np.float16)
+def cpu_baseline(cfg: str, shapes, budget_s: float = 12.0) -> dict:
+    """The reference's torch CPU matmul path, timed on this host's cores on a bounded
+    sample of the same layer: one torch.matmul(A_i, B_i.T) per problem — fp16 operands for fp16
+    problems; int-valued fp32 operands plus the reference epilogue
+    fp16(f32(acc) * f32(fp16(sa * sb))) (mm_tile.cuh:469-496) for quantised ones. Routed problems of
+    gate_up then down in call order until ~budget_s / 3 of CPU time, then 1 warm-up + 3 timed passes
+    over that sample. A reported baseline, not the optimisation target."""
+    info = cpu_info()
+    torch.set_num_threads(info["threads"])
+    g = torch.Generator().manual_seed(0)
+    sample, est = [], 0.0
+    for gg in ("gate_up", "down"):
+        for sh in shapes[gg][:-1]:
+            if sh.M == 0:
+                continue
+            if sh.qcfg == "fp16":
+                a = (torch.rand(sh.M, sh.K, generator=g) * 2 - 1).half()
+                b = (torch.rand(sh.N, sh.K, generator=g) * 2 - 1).half()
+                sa = sb = None
+            else:
+                qm = (1 << (sh.a_bits - 1)) - 1
+                a = torch.randint(-qm, qm + 1, (sh.M, sh.K), generator=g).float()
+                b = torch.randint(-qm, qm + 1, (sh.N, sh.K), generator=g).float()
+                sa = (torch.rand(sh.M, generator=g) * 0.01).half()
+                sb = (torch.rand(sh.N, generator=g) * 0.01).half()
+            sample.append((gg, sh, a, b, sa, sb))
             t0 = time.perf_counter()
-            oracle.gg_f16(A, B, M, N, K, threads)
-        else:
-            bits = s.a_bits
-            A = rng.integers(0, 256, (M, K * bits // 8), dtype=np.uint8)
-            B = rng.integers(0, 256, (N, K * bits // 8), dtype=np.uint8)
-            sa = (rng.random(M, np.float32) * 0.01).astype(np.float16)
-            sb = (rng.random(N, np.float32) * 0.01).astype(np.float16)
-            t0 = time.perf_counter()
-            oracle.gg_quant(A, B, sa, sb, M, N, K, bits, threads)
-        t_used += time.perf_counter() - t0
-        done_flops += 2 * M * N * K
-        names.append(f"{gg}[{M}x{N}x{K} {s.qcfg}]")
-        if t_used > budget_s:
+            one_problem(a, b, sa, sb)
+            est += time.perf_counter() - t0
+            if est > budget_s / 3:
+                break
+        if est > budget_s / 3:
             break
+
+    def run_pass():
+        for _, _, a, b, sa, sb in sample:
+            one_problem(a, b, sa, sb)
+
+    run_pass()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(3):
+        run_pass()
+    dt = (time.perf_counter() - t0) / 3
+    flops = sum(2 * sh.M * sh.N * sh.K for _, sh, *_ in sample)
+    names = [f"{gg}[{sh.M}x{sh.N}x{sh.K} {sh.qcfg}]" for gg, sh, *_ in sample]
     shown = ", ".join(names[:3]) + (f", ... ({len(names) - 3} more)" if len(names) > 3 else "")
-    return {"value": round(done_flops / t_used / 1e12, 6), "unit": "TFLOP/s", "cores": threads, "kind": "port",
-            "sample": f"first {len(names)} routed-expert problems of the same layer in call order ({shown}); "
-                      f"{done_flops / 1e9:.1f} GFLOP in {t_used:.1f} s; oracle/gg_oracle.c, OpenMP "
-                      f"{threads} threads, {platform.machine()}"}
+    return {"value": round(flops / dt / 1e12, 6), "unit": "TFLOP/s", "cores": info["threads"], "kind": "port",
+            "impl": "torch.matmul(A_i, B_i.T) per problem on the host (the reference's torch CPU matmul path); "
+                    + ("fp16 operands" if cfg == "fp16" else "int-valued fp32 operands + fp16 scale epilogue"),
+            "cpu_model": info["model"], "threads": info["threads"], "visible_cpus": info["visible_cpus"],
+            "sample": f"{len(sample)} routed-expert problems of the same layer in call order ({shown}); "
+                      f"{flops / 1e9:.1f} GFLOP per pass, 1 warm-up + 3 timed passes, {dt * 1e3:.0f} ms per pass"}
+
+
+def one_problem(a, b, sa, sb):
+    """One problem of the CPU baseline: C = A . B^T (+ the quantised epilogue)."""
+    acc = torch.matmul(a, b.t())
+    if sa is None:
+        return acc
+    s16 = (sa.float()[:, None] * sb.float()[None, :]).half().float()
+    return (acc * s16).half()
 
 
 def load_pmc_traffic(cfg: str):
@@ -212,7 +255,7 @@ def main():
     ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 strong-scaling + all-gather extra")
-    ap.add_argument("--extras", default="w8a8,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
+    ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
     args = ap.parse_args()
 

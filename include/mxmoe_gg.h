@@ -143,12 +143,19 @@ int mxmoe_gg_run(const mxmoe_gg_problem* problems, int problem_count, int varian
  * generated host API groupgemm_hz_fused_<i>, kernel_sketch.py:25-46, 82-145).
  * ptr_* / problem_sizes / qbits_list are DEVICE arrays, h_problem_sizes / h_qbits_list host
  * copies; ptr_Ds and the ld* arrays are accepted and ignored exactly as in the reference.
- * Runs the default variant on the legacy default stream. Unlike the reference it reports
- * errors through the return value (and mxmoe_gg_last_error) instead of exit(). */
+ * Runs the AUTO variant on the legacy default stream. Unlike the reference it reports errors
+ * through the return value (and mxmoe_gg_last_error) instead of exit(), and validates the gathered
+ * device pointers (NULL, 16-B alignment) like mxmoe_gg_plan. It keeps one workspace and one pinned
+ * staging buffer per device (grown on demand, one host synchronisation per call); release them with
+ * mxmoe_gg_release_shim_workspaces(). */
 int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr_scale_b, void** ptr_Cs,
                     void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
                     mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
                     mxmoe_qparams* h_qbits_list, int problem_count);
+
+/* Free groupgemm_mxmoe's per-device workspaces and staging buffers (waits for each device to be
+ * idle first). Safe to call at any time; the next shim call re-allocates. */
+int mxmoe_gg_release_shim_workspaces(void);
 
 /* Weight-only (WxA16) B, host-side and once per weight: converts the reference's packed words
  * (pack_weightonly after permute_weight(Row), quantize.cuh:318-421: uint16 [N / (16/w_bits)][K],

@@ -8,6 +8,7 @@ runtime torch already loaded (one runtime per process; streams and device pointe
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 from pathlib import Path
@@ -74,7 +75,7 @@ EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
     "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
-    "groupgemm_mxmoe", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
+    "groupgemm_mxmoe", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     # include/mxmoe_moe.h (MoE-layer plumbing)
     "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_combine",
 )
@@ -117,6 +118,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.groupgemm_mxmoe.restype = c.c_int
     lib.groupgemm_mxmoe.argtypes = [c.c_void_p] * 10 + [c.c_void_p, c.POINTER(MxmoeDim3), c.c_void_p,
                                                          c.POINTER(MxmoeQParams), c.c_int]
+    lib.mxmoe_gg_release_shim_workspaces.restype = c.c_int
+    lib.mxmoe_gg_release_shim_workspaces.argtypes = []
     lib.mxmoe_gg_repack_weightonly.restype = c.c_int
     lib.mxmoe_gg_repack_weightonly.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
     lib.mxmoe_gg_debug_trace.restype = c.c_int
@@ -146,7 +149,20 @@ def lib() -> ctypes.CDLL:
         except OSError as e:  # pragma: no cover - environment dependent
             raise NativeLibraryError(f"failed to load {path}: {e}") from e
         _declare(_lib)
+        atexit.register(_release_shim)
     return _lib
+
+
+def _release_shim() -> None:
+    """Free the reference-ABI shim's per-device buffers before the HIP runtime tears down (only if
+    a GPU is present: on a CPU-only host no shim call can have allocated)."""
+    try:
+        import torch
+
+        if torch.cuda.is_initialized():
+            _lib.mxmoe_gg_release_shim_workspaces()
+    except Exception:  # pragma: no cover - interpreter shutdown
+        pass
 
 
 def check(status: int) -> None:

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -824,6 +825,59 @@ int mxmoe_gg_run(const mxmoe_gg_problem* problems, int problem_count, int varian
 
 // Reference-compatible entry point (registry.cuh:28-39): device pointer arrays, host copies of
 // the sizes and QParams, legacy default stream, per-call planning (as the reference host API).
+// Per-device resources of the reference-ABI shim (the only entry that allocates): a device
+// workspace grown on demand and a pinned host staging buffer for the pointer gather and the
+// workspace image. Keyed by the calling thread's current device; one mutex per process guards the
+// table and serialises shim calls (the reference's host API is not reentrant either, it runs
+// cudaMalloc / cudaMemcpy / cudaFree on the legacy stream every call, kernel_sketch.py:102-143).
+namespace {
+struct ShimDev {
+  void* ws = nullptr;
+  size_t ws_cap = 0;
+  uint8_t* pinned = nullptr;
+  size_t pin_cap = 0;
+};
+std::mutex g_shim_mu;
+std::vector<ShimDev> g_shim;  // indexed by device ordinal
+
+int shim_grow(ShimDev& d, size_t ws_bytes, size_t pin_bytes) {
+  if ((d.ws_cap < ws_bytes && d.ws) || (d.pin_cap < pin_bytes && d.pinned))
+    HIP_TRY(hipStreamSynchronize(nullptr));  // a previous shim copy / launch may still use the old buffer
+  if (d.ws_cap < ws_bytes) {
+    if (d.ws) HIP_TRY(hipFree(d.ws));
+    d.ws = nullptr;
+    d.ws_cap = 0;
+    HIP_TRY(hipMalloc(&d.ws, ws_bytes));
+    d.ws_cap = ws_bytes;
+  }
+  if (d.pin_cap < pin_bytes) {
+    if (d.pinned) HIP_TRY(hipHostFree(d.pinned));
+    d.pinned = nullptr;
+    d.pin_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&d.pinned, pin_bytes, hipHostMallocDefault));
+    d.pin_cap = pin_bytes;
+  }
+  return MXMOE_GG_OK;
+}
+}  // namespace
+
+int mxmoe_gg_release_shim_workspaces(void) {
+  std::lock_guard<std::mutex> lk(g_shim_mu);
+  int dev0 = 0;
+  HIP_TRY(hipGetDevice(&dev0));
+  for (size_t i = 0; i < g_shim.size(); ++i) {
+    ShimDev& d = g_shim[i];
+    if (!d.ws && !d.pinned) continue;
+    HIP_TRY(hipSetDevice((int)i));
+    HIP_TRY(hipDeviceSynchronize());  // the last shim launch on this device may still read the workspace
+    if (d.ws) HIP_TRY(hipFree(d.ws));
+    if (d.pinned) HIP_TRY(hipHostFree(d.pinned));
+    d = ShimDev{};
+  }
+  HIP_TRY(hipSetDevice(dev0));
+  return MXMOE_GG_OK;
+}
+
 int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr_scale_b, void** ptr_Cs,
                     void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
                     mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
@@ -837,43 +891,57 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
   (void)qbits_list;
   if (problem_count < 0 || !h_problem_sizes || !h_qbits_list)
     return fail(MXMOE_GG_ERR_INVALID, "bad arguments to groupgemm_mxmoe");
+  if (problem_count == 0) return MXMOE_GG_OK;
+  void** src[5] = {ptr_As, ptr_Bs, ptr_scale_a, ptr_scale_b, ptr_Cs};
+  for (int c = 0; c < 5; ++c)
+    if (!src[c]) return fail(MXMOE_GG_ERR_INVALID, "groupgemm_mxmoe: NULL device pointer array");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_shim_mu);
+  if ((int)g_shim.size() <= dev) g_shim.resize(dev + 1);
+  ShimDev& d = g_shim[dev];
+  // 1. gather the caller's device pointer arrays: 5 async copies into pinned memory, ONE sync (the
+  //    reference pays one blocking cudaMemcpy per call, kernel_sketch.py:102-104)
+  const size_t col = (size_t)problem_count * sizeof(void*);
+  int st = shim_grow(d, 0, 5 * col);
+  if (st) return st;
+  for (int c = 0; c < 5; ++c)
+    HIP_TRY(hipMemcpyAsync(d.pinned + c * col, src[c], col, hipMemcpyDeviceToHost, nullptr));
+  HIP_TRY(hipStreamSynchronize(nullptr));
+  void* const* h = reinterpret_cast<void* const*>(d.pinned);
   std::vector<HostProblem> hp(problem_count);
   for (int i = 0; i < problem_count; ++i)
-    hp[i] = HostProblem{nullptr, nullptr, nullptr, nullptr, nullptr, (int)h_problem_sizes[i].x,
+    hp[i] = HostProblem{h[0 * problem_count + i], h[1 * problem_count + i], h[2 * problem_count + i],
+                        h[3 * problem_count + i], h[4 * problem_count + i], (int)h_problem_sizes[i].x,
                         (int)h_problem_sizes[i].y, (int)h_problem_sizes[i].z, h_qbits_list[i].a_bits,
                         h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0};
+  // 2. plan with the same NULL / alignment checks as mxmoe_gg_plan (a bad pointer is an error code,
+  //    never a fault inside the LDS-DMA kernel)
   int variant;
-  int st = resolve_variant(MXMOE_GG_VARIANT_AUTO, hp, &variant);
+  st = resolve_variant(MXMOE_GG_VARIANT_AUTO, hp, &variant);
   if (st) return st;
   Plan plan;
-  st = plan_host(hp, variant, false, &plan);
+  st = plan_host(hp, variant, true, &plan);
   if (st) return st;
   if (plan.total_tiles == 0) return MXMOE_GG_OK;
-  // gather the caller's device pointer arrays through the host (same sync cost class as the
-  // reference's per-call cudaMemcpy, kernel_sketch.py:102-104)
-  std::vector<void*> h[5];
-  void** src[5] = {ptr_As, ptr_Bs, ptr_scale_a, ptr_scale_b, ptr_Cs};
-  for (int c = 0; c < 5; ++c) {
-    h[c].resize(problem_count);
-    HIP_TRY(hipMemcpy(h[c].data(), src[c], problem_count * sizeof(void*), hipMemcpyDeviceToHost));
-  }
   std::vector<const void*> cols[5];
-  for (int r : plan.order)
-    for (int c = 0; c < 5; ++c) cols[c].push_back(h[c][r]);
+  for (int r : plan.order) {
+    cols[0].push_back(hp[r].A);
+    cols[1].push_back(hp[r].B);
+    cols[2].push_back(hp[r].SA);
+    cols[3].push_back(hp[r].SB);
+    cols[4].push_back(hp[r].C);
+  }
   WsLayout l;
   std::vector<uint8_t> img = workspace_image(plan, cols, &l);
-  thread_local void* ws = nullptr;
-  thread_local size_t ws_cap = 0;
-  if (ws_cap < l.total) {
-    if (ws) HIP_TRY(hipFree(ws));
-    ws = nullptr;
-    ws_cap = 0;
-    HIP_TRY(hipMalloc(&ws, l.total));
-    ws_cap = l.total;
-  }
-  HIP_TRY(hipMemcpy(ws, img.data(), img.size(), hipMemcpyHostToDevice));
+  // 3. upload from pinned memory and launch, both on the legacy stream, no further host sync: the
+  //    next shim call on this device synchronises that stream before it rewrites either buffer
+  st = shim_grow(d, l.total, std::max(5 * col, img.size()));
+  if (st) return st;
+  memcpy(d.pinned, img.data(), img.size());
+  HIP_TRY(hipMemcpyAsync(d.ws, d.pinned, img.size(), hipMemcpyHostToDevice, nullptr));
   mxmoe_gg_plan_info info;
-  fill_info(plan, variant, l, ws, &info);
+  fill_info(plan, variant, l, d.ws, &info);
   return mxmoe_gg_launch(&info, nullptr);
 }
 

@@ -225,3 +225,40 @@ def test_64bit_offsets_large_c(q):
         assert torch.allclose(got, ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
     del C
     torch.cuda.empty_cache()
+
+
+def _shim_call(hps):
+    def ptrs(get):
+        return torch.tensor([get(h.problem) for h in hps], dtype=torch.int64, device=DEV)
+
+    groupgemm_reference_abi(
+        ptrs(lambda p: p.A.data_ptr()), ptrs(lambda p: p.B.data_ptr()),
+        ptrs(lambda p: 0 if p.scale_a is None else p.scale_a.data_ptr()),
+        ptrs(lambda p: 0 if p.scale_b is None else p.scale_b.data_ptr()), ptrs(lambda p: p.C.data_ptr()),
+        [(h.M, h.N, h.K) for h in hps], [h.q for h in hps])
+
+
+def test_reference_abi_shim_growing_problem_count_and_release():
+    """The shim's cached per-device workspace grows between calls (P 2 -> 9, more tiles) and is
+    released explicitly; every call's output is exact."""
+    small = [HostProblem(33, 128, 256, W8A8, seed=61, device=DEV), HostProblem(17, 128, 128, FP16, seed=62, device=DEV)]
+    _shim_call(small)
+    torch.cuda.synchronize()
+    _check(small)
+    big = [HostProblem(300 + 40 * i, 512, 512, [W8A8, W4A4, FP16][i % 3], seed=70 + i, device=DEV) for i in range(9)]
+    _shim_call(big)
+    _shim_call(small)  # back to the small plan on the grown buffers
+    torch.cuda.synchronize()
+    _check(big)
+    _check(small)
+    nat.check(nat.lib().mxmoe_gg_release_shim_workspaces())
+    _shim_call(small)  # re-allocates after a release
+    torch.cuda.synchronize()
+    _check(small)
+
+
+def test_reference_abi_shim_rejects_null_scale():
+    hps = [HostProblem(33, 128, 256, W8A8, seed=81, device=DEV)]
+    hps[0].problem.scale_b = None  # the gathered pointer is NULL: an error code, not a GPU fault
+    with pytest.raises(nat.GGError, match="NULL scale"):
+        _shim_call(hps)

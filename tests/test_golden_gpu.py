@@ -102,14 +102,20 @@ def _sample_check(inputs, n_rows=48, n_cols=48, seed=0):
 
 
 @pytest.mark.parametrize("variant", [v for v in nat.production_variants() if v >= 3] + [0])
-@pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed"])
+@pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed", "ds2_mixed"])
 def test_full_size_layer11_sampled_parity(cfg, variant):
+    """BASELINE configs[1]-[4] at full size (bs=8192): qwen2_moe layer 11 fp16 / w8a8 / w4a4 / LP-1
+    mixed, and the DeepSeek-V2-Lite mixed w4a4+w8a8 layer (64 routed + 2 shared experts)."""
     from mxmoe_amd.harness import build_layer_inputs
-    from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+    from mxmoe_amd.workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1,
+                                    qwen2_layer11_workload)
 
-    kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
-          "mixed": dict(qconfig=mixed_qconfig_lp1())}[cfg]
-    wl = load_workload(qwen2_layer11_workload(8192, **kw))["layer-11"]
+    if cfg == "ds2_mixed":
+        wl = load_workload(ds2_workload(8192, qconfig=ds2_mixed_qconfig()))["layer-1"]
+    else:
+        kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
+              "mixed": dict(qconfig=mixed_qconfig_lp1())}[cfg]
+        wl = load_workload(qwen2_layer11_workload(8192, **kw))["layer-11"]
     for gg in ("gate_up", "down"):
         inp = build_layer_inputs(wl[gg])
         ggm = GroupGemm(inp.problems, variant=variant)
