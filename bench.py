@@ -6,12 +6,13 @@ One "step" = one pass of the hot path over one batch: the layer's two fused Grou
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config fp16|w8a8|w4a4|mixed] [--variant V]
   (N > 1: launched by torch.distributed.run, one rank per GPU)
 
-Multi-GPU (weak scaling, expert parallel): with N ranks the global batch is N x 8192 tokens and the
-routed experts are sharded by index across ranks (LPT on expert cost); rank r runs its experts with
-M = N * M_e rows (the tokens routed to them from the whole global batch) plus the replicated shared
-expert on its local 8192 tokens. Per-rank work stays ~ one layer; there is no collective inside the
-GroupGEMM (token dispatch/combine is MoE-layer plumbing outside this path).
-value = FLOPs of all ranks / max-over-ranks time of K steps.
+Multi-GPU (strong scaling): with N ranks the SAME layer is split by dist.nslice_plan
+into (problem, N-slice) work items, LPT-assigned (the shared expert — half of each call's FLOPs — is
+N-split); every rank writes its C slices into one packed shard and the shards are all-gathered over
+RCCL / xGMI, the gate_up gather on a second stream while down computes. value = the layer's FLOPs /
+max-over-ranks time of K such steps. extras.strong_scaling carries T1, compute-only and serial
+(no-overlap) times and both speedups; extras.ep_weak_scaling the expert-parallel weak-scaling
+number (N x 8192 tokens, no collective).
 """
 from __future__ import annotations
 
@@ -82,74 +83,61 @@ def full_layer(cfg: str, bs: int = 8192):
     return load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
 
 
-def strong_scaling_rccl(cfg: str, dev, world: int, rank: int, steps: int = 10, warmup: int = 3, coll_dev=None) -> dict:
-    """Strong scaling of one layer's calls over the node, measured for real at N > 1:
-    every rank holds the full inputs (activations and weights replicated, same seeds), runs its
-    dist.nslice_plan work list with each C slice written straight into a packed local shard, then
-    one all_gather_into_tensor over RCCL / xGMI. Reports T1 (the full call on each GPU, max over
-    ranks), compute-only time (max over ranks) and compute + all-gather."""
-    import dataclasses
-    import time
-
+def strong_scaling_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int, coll_dev, variant=None,
+                        median_iters: int = 50) -> dict:
+    """The N > 1 headline (SURVEY.md §8e, strong scaling): ONE layer (the N = 1 workload) split over
+    the ranks by dist.nslice_plan. Every rank holds the full inputs (same seeds), runs its work list
+    with its C slices packed into one local shard, and the shards are all-gathered over RCCL / xGMI;
+    the gate_up gather runs on a second stream while down computes (dist.ShardedLayerStep).
+    Timed K steps between barriers + synchronisations, max over ranks, for: the full layer on one GPU
+    (T1, every rank), the sharded compute only, and compute + all-gathers (the step)."""
     import torch.distributed as dist
 
-    from mxmoe_amd.dist import nslice_plan, shard_bytes
+    from mxmoe_amd.dist import ShardedCall, ShardedLayerStep
     from mxmoe_amd.groupgemm import GroupGemm
-    from mxmoe_amd.harness import build_layer_inputs, slice_scale_b
+    from mxmoe_amd.harness import build_layer_inputs, time_launches
 
-    def timed(fn):
-        for _ in range(warmup):
+    layer = full_layer(cfg)
+    inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down")) for gg in ("gate_up", "down")}
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn, k=steps, w=warmup):
+        for _ in range(w):
             fn()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(dev)
         dist.barrier()
+        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(steps):
+        for _ in range(k):
             fn()
-        torch.cuda.synchronize()
-        t = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], dtype=torch.float64, device=coll_dev or dev)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    out = {}
-    layer = full_layer(cfg)
-    for gg in ("gate_up", "down"):
-        inp = build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down"))
-        full = GroupGemm(inp.problems, device=dev)
-        t1 = timed(full.launch)
-        plan = nslice_plan(inp.shapes, world)
-        pad = max(shard_bytes(inp.shapes, w) for w in plan)
-        local = torch.empty(pad, dtype=torch.float16, device=dev)
-        gathered = torch.empty(world * pad, dtype=torch.float16, device=dev)
-        mine, off = [], 0
-        for w in plan[rank]:
-            p = inp.problems[w.problem]
-            n = p.M * w.width
-            mine.append(dataclasses.replace(p, B=p.B[w.n0:w.n1], N=w.width, ldc=0,
-                                            C=local[off:off + n].view(max(p.M, 1), w.width),
-                                            scale_b=slice_scale_b(p, w.n0, w.n1)))
-            off += n
-        part = GroupGemm(mine, device=dev) if mine else None
-
-        def compute():
-            if part is not None:
-                part.launch()
-
-        def e2e():
-            compute()
-            if (coll_dev or dev).type == "cuda":
-                dist.all_gather_into_tensor(gathered, local)
-            else:  # gloo rehearsal: stage through host memory
-                g = torch.empty(gathered.numel(), dtype=gathered.dtype)
-                dist.all_gather_into_tensor(g, local.cpu())
-                gathered.copy_(g)
-
-        tc, te = timed(compute), timed(e2e)
-        out[gg] = {"t1_ms": round(t1, 4), "compute_ms": round(tc, 4), "compute_allgather_ms": round(te, 4),
-                   "speedup_compute": round(t1 / tc, 3), "speedup_with_allgather": round(t1 / te, 3),
-                   "allgather_MB_per_rank": round(2 * pad / 1e6, 1)}
-        del inp, full, part, local, gathered
-        torch.cuda.empty_cache()
-    return out
+    full = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
+    t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)))
+    del full
+    calls = {gg: ShardedCall(inp[gg], world, rank, variant=variant) for gg in inp}
+    step = ShardedLayerStep(calls["gate_up"], calls["down"], overlap=True)
+    serial = ShardedLayerStep(calls["gate_up"], calls["down"], overlap=False)
+    t_comp = timed(lambda: step.compute_only(stream))
+    t_serial = timed(lambda: serial(stream))
+    t_step = timed(lambda: step(stream))
+    flops = float(inp["gate_up"].flops + inp["down"].flops)
+    per = {gg: (time_launches(lambda g=gg: calls[g].compute(stream), warmup=3, iters=median_iters, stream=stream)
+                if calls[gg].part is not None else {"mean_ms": 0.0, "median_ms": 0.0}) for gg in calls}
+    return {"dt": t_step, "total_flops": flops, "t1": t1, "t_compute": t_comp, "t_serial": t_serial,
+            "per": per, "flops_local": {gg: calls[gg].flops_local for gg in calls},
+            "bytes_local": {gg: sum(calls[gg].shapes[w.problem].M * w.width * 2 +
+                                    (calls[gg].shapes[w.problem].M + w.width) * calls[gg].shapes[w.problem].K *
+                                    (16 if calls[gg].shapes[w.problem].qcfg == "fp16" else calls[gg].shapes[w.problem].a_bits) // 8
+                                    for w in calls[gg].plan[rank]) for gg in calls},
+            "allgather_MB_per_rank": {gg: round(2 * calls[gg].pad * (world - 1) / 1e6, 1) for gg in calls},
+            "variant": calls["gate_up"].part.variant if calls["gate_up"].part is not None else -1,
+            "tiles": {gg: calls[gg].part.total_tiles if calls[gg].part is not None else 0 for gg in calls}}
 
 
 def cpu_info() -> dict:
@@ -331,15 +319,47 @@ def main():
         return res
 
     cfg = args.config
-    main_res = run_config(cfg, args.steps, args.warmup, True)
     peak = PEAK_TFLOPS[CONFIGS[cfg]["peak"]]
+    extras = {}
+    if world == 1:
+        main_res = run_config(cfg, args.steps, args.warmup, True)
+        f_gu, f_dn = main_res["flops"]["gate_up"], main_res["flops"]["down"]
+        b_step = main_res["bytes"]["gate_up"] + main_res["bytes"]["down"]
+    else:
+        # strong scaling of ONE layer over the node (the verdict's N > 1 headline): value = the
+        # layer's FLOPs / max-rank time of compute + RCCL all-gathers (gate_up gather overlapped)
+        sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev,
+                                   variant=args.variant if args.variant >= 0 else None, median_iters=args.median_iters)
+        main_res = {"dt": sres["dt"], "total_flops": sres["total_flops"], "per": sres["per"],
+                    "flops": sres["flops_local"], "variant": sres["variant"], "tiles": sres["tiles"],
+                    "shapes": full_layer(cfg)}
+        f_gu, f_dn = sres["flops_local"]["gate_up"], sres["flops_local"]["down"]
+        b_step = sres["bytes_local"]["gate_up"] + sres["bytes_local"]["down"]
+        ms = lambda t: t / args.steps * 1e3  # noqa: E731
+        extras["strong_scaling"] = {
+            "what": "one layer split by dist.nslice_plan over the ranks; T1 = the whole layer on one GPU (max over "
+                    "ranks), compute = max-rank time of the local work lists, step = compute + RCCL "
+                    "all_gather_into_tensor of the packed C shards with the gate_up gather on a second stream "
+                    "beside the down call (value), serial = the same without the overlap",
+            "t1_ms": round(ms(sres["t1"]), 4), "compute_ms": round(ms(sres["t_compute"]), 4),
+            "step_ms": round(ms(sres["dt"]), 4), "serial_ms": round(ms(sres["t_serial"]), 4),
+            "speedup_compute": round(sres["t1"] / sres["t_compute"], 3),
+            "speedup_with_allgather": round(sres["t1"] / sres["dt"], 3),
+            "allgather_MB_received_per_rank": sres["allgather_MB_per_rank"]}
+        try:  # the round-1 headline, kept as an extra: expert-parallel weak scaling, no collective
+            ep = run_config(cfg, args.steps, args.warmup, True)
+            extras["ep_weak_scaling"] = {
+                "what": "global batch N x 8192 tokens, routed experts sharded by index (LPT), shared expert "
+                        "replicated on local tokens; no collective (dispatch / combine is MoE plumbing)",
+                "value_tflops": round(ep["total_flops"] * args.steps / ep["dt"] / 1e12, 3),
+                "ms_per_step": round(ep["dt"] / args.steps * 1e3, 4)}
+        except Exception as e:  # an extra must not lose the headline
+            extras["ep_weak_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     per = main_res["per"]
-    f_gu, f_dn = main_res["flops"]["gate_up"], main_res["flops"]["down"]
     t_gu, t_dn = per["gate_up"]["mean_ms"], per["down"]["mean_ms"]
     achieved = (f_gu + f_dn) / ((t_gu + t_dn) * 1e-3) / 1e12
-    # roofline of the step's two launches: MFMA-bound unless the arithmetic intensity puts the
-    # HBM roof (algorithmic bytes x 8 TB/s) below the MFMA peak (small batches, weight-only)
-    b_step = main_res["bytes"]["gate_up"] + main_res["bytes"]["down"]
+    # roofline of the step's two launches (this rank's at N > 1): MFMA-bound unless the arithmetic
+    # intensity puts the HBM roof (algorithmic bytes x 8 TB/s) below the MFMA peak
     if (f_gu + f_dn) / b_step * HBM_GBS / 1e3 < peak:
         gbs = b_step / ((t_gu + t_dn) * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_GBS, "unit": "GB/s", "frac": round(gbs / HBM_GBS, 4),
@@ -350,8 +370,7 @@ def main():
     value = main_res["total_flops"] * args.steps / main_res["dt"] / 1e12
     pmc = load_pmc_traffic(cfg) if world == 1 else None  # the committed PMC passes are single-GPU runs
 
-    extras = {}
-    if rank == 0:
+    if rank == 0 and world == 1:
         for gg in ("gate_up", "down"):
             b = main_res["bytes"][gg]
             f = main_res["flops"][gg]
@@ -392,16 +411,6 @@ def main():
             "gate_up_ms": asref["gate_up"], "down_ms": asref["down"],
             "tflops": round((f["gate_up"] + f["down"]) / ((asref["gate_up"] + asref["down"]) * 1e-3) / 1e12, 2)}
 
-    if world > 1 and not args.no_strong_scaling:
-        try:
-            extras["strong_scaling_rccl"] = {
-                "what": "one layer's calls split by dist.nslice_plan over the node: T1 = full call per GPU, "
-                        "compute = max-rank time of the local work list, + RCCL all_gather_into_tensor of "
-                        "the packed C shards (wall ms, max over ranks)",
-                **strong_scaling_rccl(cfg, dev, world, rank, coll_dev=coll_dev)}
-        except Exception as e:  # a failure here must not lose the weak-scaling line
-            extras["strong_scaling_rccl"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, main_res["shapes"])
@@ -416,17 +425,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(main_res["dt"] / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": CONFIGS[cfg]["dtype"],
             "data": "synthetic: uniform(-1,1) fp16 inputs (seeded) -> RTN per-row quantised + pack_wxax for "
                     "quantised problems; routed M_e = " + ("reference's committed bs=8192 histogram"
                                                          if not cfg.startswith("ds2") else
                                                          "seeded multinomial (SURVEY.md 8d)"),
-            "config": {"workload": CONFIGS[cfg]["name"] + (f", expert-parallel over {world} GPUs" if world > 1 else ""),
+            "config": {"workload": CONFIGS[cfg]["name"] + (f", one layer split over {world} GPUs (N-slices + RCCL "
+                                                          f"all-gather of C)" if world > 1 else ""),
                        "model": ("DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")
-                       + " MoE GroupGEMMs", "global_batch": CONFIGS[cfg].get("bs", 8192) * world,
-                       "seq_len": None, "parallelism": f"ep{world}" if world > 1 else "single",
+                       + " MoE GroupGEMMs", "global_batch": CONFIGS[cfg].get("bs", 8192),
+                       "seq_len": None, "parallelism": f"nslice{world}+allgather" if world > 1 else "single",
                        "problems_per_call": len(main_res["shapes"]["gate_up"]), "variant": main_res["variant"],
                        "variant_name": nat.list_variants()[main_res["variant"]].split()[1]},
             "roofline": {**roof,

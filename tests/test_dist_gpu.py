@@ -1,0 +1,75 @@
+"""The N > 1 bench path on the GPU: dist.ShardedCall / ShardedLayerStep with 2 ranks sharing the one
+GPU of the box (gloo collectives staged through host memory; the node runs use RCCL). The gathered,
+scattered layer output must equal one full single-GPU call (bit-exact on the integer paths)."""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import numpy as np
+
+        from mxmoe_amd.dist import ShardedCall, ShardedLayerStep
+        from mxmoe_amd.groupgemm import GroupGemm
+        from mxmoe_amd.harness import build_layer_inputs
+        from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        kw = {"fp16": {}, "mixed": dict(qconfig=mixed_qconfig_lp1())}[cfg]
+        layer = load_workload(qwen2_layer11_workload(1024, **kw))["layer-11"]
+        inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=7 + (gg == "down")) for gg in ("gate_up", "down")}
+        calls = {gg: ShardedCall(inp[gg], world, rank) for gg in inp}
+        step = ShardedLayerStep(calls["gate_up"], calls["down"])
+        s = torch.cuda.current_stream(dev)
+        step(s)
+        torch.cuda.synchronize(dev)
+        ok = True
+        for gg in inp:
+            outs = [torch.full_like(p.C, float("nan")) for p in inp[gg].problems]
+            calls[gg].scatter(outs)
+            GroupGemm(inp[gg].problems).launch(s)  # the reference: one full call on this GPU
+            torch.cuda.synchronize(dev)
+            for p, o in zip(inp[gg].problems, outs):
+                a, b = o[: p.M].cpu().numpy(), p.C[: p.M].cpu().numpy()
+                if p.q.is_quant:
+                    ok &= bool(np.array_equal(a.view(np.uint16), b.view(np.uint16)))
+                else:
+                    ok &= bool(np.allclose(a.astype(np.float64), b.astype(np.float64), rtol=2e-3, atol=2e-3))
+        q.put((rank, ok, calls["gate_up"].pad > 0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", ["mixed", "fp16"])
+def test_sharded_layer_step_matches_full_call(cfg):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
