@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-PEAK_TFLOPS = {"fp16": 2500.0, "int8": 5000.0}  # dense MFMA peaks, MI355X_MICROARCH.md (spec)
+PEAK_TFLOPS = {"fp16": 2500.0, "int8": 5000.0, "fp8": 5000.0}  # dense MFMA peaks, MI355X_MICROARCH.md (spec)
 HBM_GBS = 8000.0
 
 CONFIGS = {
@@ -55,6 +55,20 @@ CONFIGS = {
                         name="qwen2_moe layer-11 w2a16_g128_asym GroupGEMM bs=512 (weight-bandwidth bound)"),
     "fp16_bs512": dict(kw={}, peak="fp16", dtype="fp16", bs=512,
                        name="qwen2_moe layer-11 fp16 GroupGEMM bs=512"),
+    # the reference's other SUPPORTED_QCFG strategies (tile_config.py:40-106)
+    "w8a8_e4m3": dict(kw=dict(qstr="w8a8_g-1_sym_E4M3"), peak="fp8", dtype="fp8 e4m3",
+                      name="qwen2_moe layer-11 w8a8_g-1_sym_E4M3 GroupGEMM bs=8192 (fp8 MFMA, f32 accumulate)"),
+    "bf16": dict(kw=dict(qstr="bf16"), peak="fp16", dtype="bf16",
+                 name="qwen2_moe layer-11 bf16 GroupGEMM bs=8192"),
+    # the reference CLI's other models (gen_workload.py:16-21), seeded synthetic routing
+    "mixtral_fp16": dict(kw={}, model="mixtral", peak="fp16", dtype="fp16",
+                         name="Mixtral-8x7B MoE layer fp16 GroupGEMM bs=8192 (8 experts, top-2)"),
+    "mixtral_w8a8": dict(kw=dict(qstr="w8a8_g-1_sym"), model="mixtral", peak="int8", dtype="int8",
+                         name="Mixtral-8x7B MoE layer w8a8_g-1_sym GroupGEMM bs=8192"),
+    "qwen2_57b_fp16": dict(kw={}, model="qwen2_moe_57b", peak="fp16", dtype="fp16",
+                           name="Qwen2-57B-A14B MoE layer fp16 GroupGEMM bs=8192 (64 experts, top-8, shared)"),
+    "qwen2_57b_w8a8": dict(kw=dict(qstr="w8a8_g-1_sym"), model="qwen2_moe_57b", peak="int8", dtype="int8",
+                           name="Qwen2-57B-A14B MoE layer w8a8_g-1_sym GroupGEMM bs=8192"),
 }
 
 
@@ -72,10 +86,12 @@ def layer_shapes(cfg: str, world: int, rank: int, bs: int = 8192):
 def full_layer(cfg: str, bs: int = 8192):
     """The config's whole layer {gate_up, down} (one GPU's worth at N = 1)."""
     from mxmoe_amd.workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1,
-                                    qwen2_layer11_workload)
+                                    model_workload, qwen2_layer11_workload)
 
     bs = CONFIGS[cfg].get("bs", bs)
     kw = CONFIGS[cfg]["kw"]
+    if "model" in CONFIGS[cfg]:
+        return load_workload(model_workload(CONFIGS[cfg]["model"], bs, **kw))["layer-1"]
     if kw == "ds2_mixed":
         return load_workload(ds2_workload(bs, qconfig=ds2_mixed_qconfig()))["layer-1"]
     if kw == "mixed":
@@ -172,10 +188,16 @@ def cpu_baseline(cfg: str, shapes, budget_s: float = 12.0) -> dict:
         for sh in shapes[gg][:-1]:
             if sh.M == 0:
                 continue
-            if sh.qcfg == "fp16":
-                a = (torch.rand(sh.M, sh.K, generator=g) * 2 - 1).half()
-                b = (torch.rand(sh.N, sh.K, generator=g) * 2 - 1).half()
+            if sh.qcfg in ("fp16", "bf16"):
+                dt = torch.bfloat16 if sh.qcfg == "bf16" else torch.float16
+                a = (torch.rand(sh.M, sh.K, generator=g) * 2 - 1).to(dt)
+                b = (torch.rand(sh.N, sh.K, generator=g) * 2 - 1).to(dt)
                 sa = sb = None
+            elif sh.fmt == "E4M3":  # decoded fp8 values as fp32 operands (exact), then the epilogue
+                a = (torch.rand(sh.M, sh.K, generator=g) * 2 - 1).mul(448).to(torch.float8_e4m3fn).float()
+                b = (torch.rand(sh.N, sh.K, generator=g) * 2 - 1).mul(448).to(torch.float8_e4m3fn).float()
+                sa = (torch.rand(sh.M, generator=g) * 0.01).half()
+                sb = (torch.rand(sh.N, generator=g) * 0.01).half()
             else:
                 qm = (1 << (sh.a_bits - 1)) - 1
                 a = torch.randint(-qm, qm + 1, (sh.M, sh.K), generator=g).float()
@@ -205,7 +227,10 @@ def cpu_baseline(cfg: str, shapes, budget_s: float = 12.0) -> dict:
     shown = ", ".join(names[:3]) + (f", ... ({len(names) - 3} more)" if len(names) > 3 else "")
     return {"value": round(flops / dt / 1e12, 6), "unit": "TFLOP/s", "cores": info["threads"], "kind": "port",
             "impl": "torch.matmul(A_i, B_i.T) per problem on the host (the reference's torch CPU matmul path); "
-                    + ("fp16 operands" if cfg == "fp16" else "int-valued fp32 operands + fp16 scale epilogue"),
+                    + {"fp16": "fp16 operands", "bf16": "bf16 operands",
+                       "w8a8_e4m3": "decoded e4m3 values as fp32 operands + fp16 scale epilogue"}.get(
+                        cfg.split("_", 1)[1] if cfg.startswith(("mixtral_", "qwen2_57b_")) else cfg,
+                        "int-valued fp32 operands + fp16 scale epilogue"),
             "cpu_model": info["model"], "threads": info["threads"], "visible_cpus": info["visible_cpus"],
             "sample": f"{len(sample)} routed-expert problems of the same layer in call order ({shown}); "
                       f"{flops / 1e9:.1f} GFLOP per pass, 1 warm-up + 3 timed passes, {dt * 1e3:.0f} ms per pass"}
@@ -430,11 +455,13 @@ def main():
             "dtype": CONFIGS[cfg]["dtype"],
             "data": "synthetic: uniform(-1,1) fp16 inputs (seeded) -> RTN per-row quantised + pack_wxax for "
                     "quantised problems; routed M_e = " + ("reference's committed bs=8192 histogram"
-                                                         if not cfg.startswith("ds2") else
+                                                         if not (cfg.startswith("ds2") or "model" in CONFIGS[cfg]) else
                                                          "seeded multinomial (SURVEY.md 8d)"),
             "config": {"workload": CONFIGS[cfg]["name"] + (f", one layer split over {world} GPUs (N-slices + RCCL "
                                                           f"all-gather of C)" if world > 1 else ""),
-                       "model": ("DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")
+                       "model": {"mixtral": "Mixtral-8x7B", "qwen2_moe_57b": "Qwen2-57B-A14B"}.get(
+                           CONFIGS[cfg].get("model"),
+                           "DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")
                        + " MoE GroupGEMMs", "global_batch": CONFIGS[cfg].get("bs", 8192),
                        "seq_len": None, "parallelism": f"nslice{world}+allgather" if world > 1 else "single",
                        "problems_per_call": len(main_res["shapes"]["gate_up"]), "variant": main_res["variant"],

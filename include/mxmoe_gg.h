@@ -9,6 +9,12 @@
  *   w8a8 : A,B int8  per-channel sym (gsize -1), exact int32 accumulate,
  *          C = fp16_rn(0.f + f32(acc) * f32(fp16_rn(sa[m] * sb[n])))
  *   w4a4 : A,B int4  per-channel sym (gsize -1), same epilogue
+ *   w4a4_g128, WxA16 weight-only: see DESIGN.md §4 / mxmoe_gg_repack_weightonly below
+ *   w8a8_g-1_sym_E4M3 (fmt MXMOE_GG_FMT_E4M3): A,B OCP fp8 e4m3 codes (one byte each, pack_wxax
+ *          8-bit byte order), per-channel fp16 scales, f32 accumulate (products exact, sum order
+ *          unspecified), C = fp16_rn(0.f + acc * f32(fp16_rn(sa[m] * sb[n])))
+ *   bf16 (fmt MXMOE_GG_FMT_BF16): A,B bf16, fp32 accumulate, C = fp16_rn(acc) (C is fp16 for every
+ *          type, as the reference's `half** ptr_Cs`)
  *
  * Data layout is byte-identical to the reference bench (SeaCatComplexes/MxMoE):
  *   - packed A/B words follow pack_wxax        (mxmoe/kernels/src/include/quantize.cuh:425-475)
@@ -35,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MXMOE_GG_ABI_VERSION 3
+#define MXMOE_GG_ABI_VERSION 4
 
 enum {
   MXMOE_GG_OK = 0,
@@ -45,14 +51,25 @@ enum {
   MXMOE_GG_ERR_HIP = 4          /* a HIP runtime call failed */
 };
 
+/* Element format of a problem's A / B beyond the bit widths (the reference's QConfig USE_FP flag,
+ * tile_config.py:192, and its MMA_BF16_FP32 / MMA_E4M3_K32 strategies, tile_config.py:87-106). */
+enum {
+  MXMOE_GG_FMT_DEFAULT = 0, /* fp16 for 16-bit operands, two's-complement integers otherwise */
+  MXMOE_GG_FMT_E4M3 = 1,    /* w8a8_g-1_sym_E4M3: OCP fp8 e4m3 codes                         */
+  MXMOE_GG_FMT_BF16 = 2     /* bf16: 16-bit operands are bfloat16                              */
+};
+
 /* Same memory layout as the reference's mxmoe::QParams (quantize.cuh:14-25):
- * int2 qbits {x = a_bits, y = w_bits}; int gsize; bool sym; padded to 16 bytes, 8-byte aligned. */
+ * int2 qbits {x = a_bits, y = w_bits}; int gsize; bool sym; padded to 16 bytes, 8-byte aligned.
+ * `fmt` sits in the byte after `sym` that the reference leaves as padding, so a reference caller
+ * that value-initialises its QParams passes MXMOE_GG_FMT_DEFAULT. */
 typedef struct mxmoe_qparams {
   int32_t a_bits;
   int32_t w_bits;
   int32_t gsize;
   uint8_t sym;
-  uint8_t pad_[3];
+  uint8_t fmt;
+  uint8_t pad_[2];
 } __attribute__((aligned(8))) mxmoe_qparams;
 
 /* Same memory layout as CUDA/HIP dim3 (x = M, y = N, z = K), as used in registry.cuh:28-39. */
@@ -70,7 +87,7 @@ typedef struct mxmoe_gg_problem {
   void* C;             /* fp16 [M][ldc]                                            */
   int32_t M, N, K;
   int32_t a_bits, w_bits, gsize, sym;
-  int32_t reserved_;
+  int32_t fmt; /* MXMOE_GG_FMT_* */
   int64_t lda, ldb, ldc;
 } mxmoe_gg_problem;
 
@@ -82,7 +99,8 @@ typedef struct mxmoe_gg_plan_info {
   int32_t grid;
   int32_t block;
   int32_t lds_bytes;
-  int32_t qtype_mask;      /* bit q set if a planned problem has quant type q (0 fp16, 1 w8a8, 2 w4a4);
+  int32_t qtype_mask;      /* bit q set if a planned problem has quant type q (0 fp16, 1 w8a8, 2 w4a4,
+                            * 3 w4a16, 4 w8a16, 5 w4a4_g128, 6 w2a16, 7 w8a8 E4M3, 8 bf16);
                             * selects the kernel specialisation at launch */
   int32_t splitk_slabs;    /* 256-KiB partial-sum slabs the plan's split-K tiles use (0: no split) */
   int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */

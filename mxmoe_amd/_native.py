@@ -24,6 +24,9 @@ MXMOE_GG_ERR_UNSUPPORTED = 2
 MXMOE_GG_ERR_WORKSPACE = 3
 MXMOE_GG_ERR_HIP = 4
 
+# operand formats (MXMOE_GG_FMT_*): fp16 / integer, OCP fp8 e4m3, bfloat16
+FMT_DEFAULT, FMT_E4M3, FMT_BF16 = 0, 1, 2
+
 
 class NativeLibraryError(RuntimeError):
     """libmxmoe_gg.so is missing or failed to load."""
@@ -41,7 +44,7 @@ class MxmoeQParams(ctypes.Structure):
     """Layout of the reference's mxmoe::QParams (quantize.cuh:14-25): int2 qbits; int gsize; bool sym."""
 
     _fields_ = [("a_bits", ctypes.c_int32), ("w_bits", ctypes.c_int32), ("gsize", ctypes.c_int32),
-                ("sym", ctypes.c_uint8), ("pad_", ctypes.c_uint8 * 3)]
+                ("sym", ctypes.c_uint8), ("fmt", ctypes.c_uint8), ("pad_", ctypes.c_uint8 * 2)]
 
 
 class MxmoeDim3(ctypes.Structure):
@@ -54,7 +57,7 @@ class GGProblemC(ctypes.Structure):
         ("scale_b", ctypes.c_void_p), ("C", ctypes.c_void_p),
         ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
         ("a_bits", ctypes.c_int32), ("w_bits", ctypes.c_int32), ("gsize", ctypes.c_int32),
-        ("sym", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+        ("sym", ctypes.c_int32), ("fmt", ctypes.c_int32),
         ("lda", ctypes.c_int64), ("ldb", ctypes.c_int64), ("ldc", ctypes.c_int64),
     ]
 

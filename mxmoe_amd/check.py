@@ -10,7 +10,9 @@ depends only on A[rows] and B[cols]), for every quant type the library runs:
     (cta_gemm.cuh:610-772) — bit exact (the fma formed in f64, where product and sum are exact);
   * weight-only WxA16: B codes unpacked from the kernel layout, dequantised exactly as the kernels
     do, fp16(fma(u - off, scale, zp)) (quantize.cuh:146-213), then an f64 GEMM — fp16 tolerance;
-  * fp16: f64 GEMM — relative 1e-3 (north_star) with a cancellation floor.
+  * w8a8 E4M3: e4m3 codes decoded, exact f64 dot products rounded to f32, the wxax epilogue — fp16
+    tolerance (the MFMA's f32 summation order is unspecified);
+  * fp16 / bf16: f64 GEMM — relative 1e-3 (north_star) with a cancellation floor.
 
 Unlike the reference's CHECK (abs tol 1.0 against an unquantised cutlass GEMM), integer paths must
 match bit for bit.
@@ -48,6 +50,14 @@ def expected_sample(p, rows: torch.Tensor, cols: torch.Tensor) -> tuple[torch.Te
         return A.double() @ Bdq.double().T, False
     if not q.is_quant:
         return A.double() @ p.B.index_select(0, cols).cpu().double().T, False
+    if q.is_fp8:
+        def dec(t):
+            return unpack_wxax(t, 8, p.K).view(torch.float8_e4m3fn).double()
+        acc = (dec(A) @ dec(p.B.index_select(0, cols).cpu()).T).float()
+        sa = p.scale_a.index_select(0, rows).cpu().float()
+        sb = p.scale_b.index_select(0, cols).cpu().float()
+        s16 = (sa[:, None] * sb[None, :]).half().float()
+        return (0.0 + acc * s16).half().double(), False
     qa = unpack_wxax(A, q.a_bits, p.K).to(torch.int64)
     qb = unpack_wxax(p.B.index_select(0, cols).cpu(), q.w_bits, p.K).to(torch.int64)
     if q.gsize == -1:

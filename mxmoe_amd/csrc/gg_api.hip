@@ -82,7 +82,7 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   } else if constexpr ((ABL & kWoAblMask) != 0) {
     launch_v2_q<ABL, 8>(a, grid, s);  // weight-only ablations: w4a16 tiles only
   } else {
-    switch (qmask & 127) {
+    switch (qmask & 511) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
       case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
       case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
@@ -92,12 +92,15 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       case 16: launch_v2_q<ABL, 16>(a, grid, s); break;  // w8a16 only
       case 32: launch_v2_q<ABL, 32>(a, grid, s); break;  // w4a4 g128 only
       case 64: launch_v2_q<ABL, 64>(a, grid, s); break;  // w2a16 only
+      case 128: launch_v2_q<ABL, 128>(a, grid, s); break;  // w8a8 E4M3 only
+      case 256: launch_v2_q<ABL, 256>(a, grid, s); break;  // bf16 only
       // any other mix: every tile body in one kernel. The staggered int bodies leave no register
       // room for that (the compiler spilled inside their K loops), so the fallback is plain v2;
       // the 2-bit weight-only body only joins it when the mix has one (it costs 12 B of prologue
       // spill there, tests/test_codegen.py)
       default:
-        if (qmask & (1 << QT_W2A16)) launch_v2_q<0, 127>(a, grid, s);
+        if (qmask & ((1 << QT_F8) | (1 << QT_BF16))) launch_v2_q<0, 511>(a, grid, s);
+        else if (qmask & (1 << QT_W2A16)) launch_v2_q<0, 127>(a, grid, s);
         else launch_v2_q<0, 63>(a, grid, s);
         break;
     }
@@ -128,7 +131,7 @@ Variant make_v0(const char* name) {
   v.geom[QT_F16] = {C16::BM, C16::BN, C16::BKB, C16::kThreads};
   v.geom[QT_I8] = {C8::BM, C8::BN, C8::BKB, C8::kThreads};
   v.geom[QT_I4] = {C4::BM, C4::BN, C4::BKB, C4::kThreads};
-  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = v.geom[QT_W2A16] = {0, 0, 0, 0};  // v2 kernels only
+  for (int q : {QT_W4A16, QT_W8A16, QT_I4G, QT_W2A16, QT_F8, QT_BF16}) v.geom[q] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = C16::kThreads;
   v.lds_bytes = FusedCfg<C16, C8, C4>::LDS_BYTES;
   v.chunk = FusedCfg<C16, C8, C4>::LDS_BYTES <= 80 * 1024 ? 64 : 32;  // workgroups per XCD at once
@@ -144,8 +147,8 @@ Variant make_v3(const char* name) {
   Variant v;
   v.name = name;
   v.kind = Kind::V3;
-  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};
-  v.geom[QT_W4A16] = v.geom[QT_W8A16] = v.geom[QT_I4G] = v.geom[QT_W2A16] = {0, 0, 0, 0};  // v2 kernels only
+  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};  // (weight-only / g128 / fp8 / bf16 cleared below)
+  for (int q : {QT_W4A16, QT_W8A16, QT_I4G, QT_W2A16, QT_F8, QT_BF16}) v.geom[q] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = CT::NT;
   v.lds_bytes = CT::LDS_BYTES;
   v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
@@ -230,7 +233,24 @@ int variant_index(const char* name) {
   return 0;
 }
 
-int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
+int qtype_of(int a_bits, int w_bits, int gsize, int sym, int fmt, int* qt) {
+  if (fmt == MXMOE_GG_FMT_E4M3) {  // w8a8_g-1_sym_E4M3 (tile_config.py:45, 104-106, 192)
+    if (a_bits == 8 && w_bits == 8 && gsize == -1 && sym) {
+      *qt = QT_F8;
+      return MXMOE_GG_OK;
+    }
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported: w%da%d_g%d_%s_E4M3 (only w8a8_g-1_sym_E4M3)",
+                w_bits, a_bits, gsize, sym ? "sym" : "asym");
+  }
+  if (fmt == MXMOE_GG_FMT_BF16) {  // bf16 (tile_config.py:42, 99-102)
+    if (a_bits == 16 && w_bits == 16) {
+      *qt = QT_BF16;
+      return MXMOE_GG_OK;
+    }
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported: w%da%d bf16 (only 16-bit bf16 operands)", w_bits,
+                a_bits);
+  }
+  if (fmt != MXMOE_GG_FMT_DEFAULT) return fail(MXMOE_GG_ERR_UNSUPPORTED, "unknown operand format %d", fmt);
   if (a_bits == 16 && w_bits == 16) {
     *qt = QT_F16;
     return MXMOE_GG_OK;
@@ -256,6 +276,7 @@ int qtype_of(int a_bits, int w_bits, int gsize, int sym, int* qt) {
 }
 
 bool is_weightonly(int qt) { return qt == QT_W4A16 || qt == QT_W8A16 || qt == QT_W2A16; }
+bool is_float16(int qt) { return qt == QT_F16 || qt == QT_BF16; }  // 16-bit operands, no scales
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -264,6 +285,7 @@ struct HostProblem {
   void* C;
   int M, N, K, a_bits, w_bits, gsize, sym;
   int64_t lda, ldb, ldc;  // 16-bit words, 0 = dense
+  int fmt;                // MXMOE_GG_FMT_*
 };
 
 // Workspace: [GGMeta x P][ptr_A x P][ptr_B x P][ptr_SA x P][ptr_SB x P][ptr_C x P][TileDesc x grid]
@@ -325,13 +347,13 @@ int build_meta_weightonly(const HostProblem& p, int idx, int qt, const Variant& 
 int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs, GGMeta* m) {
   if (p.M < 0 || p.N < 0 || p.K < 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: negative shape", idx);
   int qt = 0;
-  int st = qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt);
+  int st = qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt, &qt);
   if (st) return fail(st, "problem %d: %s", idx, g_last_error.c_str());
   if (v.geom[qt].bn == 0)
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s does not implement w%da%d (quant type not supported)",
                 idx, v.name, p.w_bits, p.a_bits);
   if (is_weightonly(qt)) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
-  const int abits = qt == QT_F16 ? 16 : p.a_bits;
+  const int abits = is_float16(qt) ? 16 : p.a_bits;
   const int64_t kbits = (int64_t)p.K * abits;
   if (kbits % 128 != 0)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d must be a multiple of %d for %d-bit data (16-B rows)", idx,
@@ -341,7 +363,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
                 idx, v.name, v.k_stage_bytes, p.K);
   if (qt == QT_I4G && p.K % 128 != 0)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: w4a4_g128 needs K %% 128 == 0 (K=%d)", idx, p.K);
-  if (qt != QT_F16 && p.K > 131072)
+  if (qt != QT_F16 && qt != QT_BF16 && qt != QT_F8 && p.K > 131072)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d exceeds the exact int32 accumulation bound 131072", idx, p.K);
   if (p.N % 8 != 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: N=%d must be a multiple of 8", idx, p.N);
   const int64_t kbytes = kbits / 8;
@@ -353,10 +375,10 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
   if (check_ptrs && p.M > 0 && p.N > 0) {  // empty problems are dropped by the planner
     if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
-    if (qt != QT_F16 && (!p.SA || !p.SB)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer", idx);
+    if (!is_float16(qt) && (!p.SA || !p.SB)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer", idx);
     if (((uintptr_t)p.A | (uintptr_t)p.B | (uintptr_t)p.C) & 15)
       return fail(MXMOE_GG_ERR_INVALID, "problem %d: A/B/C must be 16-byte aligned", idx);
-    if (qt != QT_F16 && (((uintptr_t)p.SA | (uintptr_t)p.SB) & 1))
+    if (!is_float16(qt) && (((uintptr_t)p.SA | (uintptr_t)p.SB) & 1))
       return fail(MXMOE_GG_ERR_INVALID, "problem %d: scales must be 2-byte aligned", idx);
   }
   memset(m, 0, sizeof(*m));
@@ -419,7 +441,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     std::vector<std::pair<int, int>> mt;
     for (int m0 = 0; m0 < m.M;) {
       const int rem = m.M - m0;
-      const bool small_class = m.qtype == QT_F16 || is_weightonly(m.qtype);
+      const bool small_class = is_float16(m.qtype) || is_weightonly(m.qtype);
       if (v.kind != Kind::V0 && v.tail2_bm && small_class && rem <= v.tail2_bm) {
         mt.push_back({m0, 2});
         m0 += v.tail2_bm;
@@ -469,8 +491,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       bytes = rows * 128 + cols * 64 * (m.qtype == QT_W2A16 ? 2 : m.qtype == QT_W4A16 ? 4 : 8) / 8.0;
       equiv = 2.0 * rows * cols * 64 / 128;
     } else {
-      const double kel = g.bkb * 8.0 / (m.qtype == QT_F16 ? 16 : m.qtype == QT_I8 ? 8 : 4);
-      const double rate = m.qtype == QT_F16 ? 128 : 256, fold = m.qtype == QT_I4G ? 1.25 : 1.0;
+      const double kel = g.bkb * 8.0 / (is_float16(m.qtype) ? 16 : (m.qtype == QT_I8 || m.qtype == QT_F8) ? 8 : 4);
+      const double rate = is_float16(m.qtype) ? 128 : 256, fold = m.qtype == QT_I4G ? 1.25 : 1.0;
       bytes = (rows + cols) * g.bkb;
       equiv = 2.0 * rows * cols * kel / rate * fold;
     }
@@ -599,7 +621,7 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   int mask = 0;
   for (const HostProblem& p : hp) {
     int qt;
-    if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) == MXMOE_GG_OK) mask |= 1 << qt;
+    if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt, &qt) == MXMOE_GG_OK) mask |= 1 << qt;
   }
   *out = variant_index(kDefaultVariantName);
   if (mask == (1 << QT_I4)) {
@@ -607,17 +629,17 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     // to split K (that kernel cannot)
     Plan p;
     if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == 0) *out = variant_index(kInt4Variant);
-  } else if (mask & ((1 << QT_F16) | (1 << QT_I8) | (1 << QT_I4))) {
+  } else if (mask & ((1 << QT_F16) | (1 << QT_I8) | (1 << QT_I4) | (1 << QT_F8) | (1 << QT_BF16))) {
     std::vector<std::pair<int, int64_t>> st;  // (128-B K stages, tiles) of the fp16 / w8a8 / w4a4 problems
     int64_t total = 0, f16_small = 0;         // f16_small: fp16 tiles of the 64-row class
     for (const HostProblem& p : hp) {
       int qt;
-      if (p.M <= 0 || qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, &qt) != MXMOE_GG_OK) continue;
-      if (qt != QT_F16 && qt != QT_I8 && qt != QT_I4) continue;
+      if (p.M <= 0 || qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt, &qt) != MXMOE_GG_OK) continue;
+      if (qt != QT_F16 && qt != QT_I8 && qt != QT_I4 && qt != QT_F8 && qt != QT_BF16) continue;
       const int64_t nt = (p.N + 255) / 256, tiles = (int64_t)((p.M + 255) / 256) * nt;
       st.emplace_back((int)(((int64_t)p.K * p.a_bits / 8 + 127) / 128), tiles);
       total += tiles;
-      if (qt == QT_F16 && p.M % 256 > 0 && p.M % 256 <= 64) f16_small += nt;
+      if (is_float16(qt) && p.M % 256 > 0 && p.M % 256 <= 64) f16_small += nt;
     }
     // low-fill fp16 calls (most tiles are 64-row remainders, e.g. bs=512 routed experts): those
     // tiles wait on their B stream, and the deeper B ring pays (+5-9 %, session3/exp_b3_bs512.jsonl)
@@ -643,7 +665,7 @@ std::vector<HostProblem> to_host(const mxmoe_gg_problem* problems, int problem_c
   for (int i = 0; i < problem_count; ++i) {
     const mxmoe_gg_problem& p = problems[i];
     hp[i] = HostProblem{p.A,      p.B,      p.scale_a, p.scale_b, p.C,   p.M,   p.N,  p.K,
-                        p.a_bits, p.w_bits, p.gsize,   p.sym,     p.lda, p.ldb, p.ldc};
+                        p.a_bits, p.w_bits, p.gsize,   p.sym,     p.lda, p.ldb, p.ldc, p.fmt};
   }
   return hp;
 }
@@ -699,8 +721,9 @@ int mxmoe_gg_default_variant(void) { return variant_index(kDefaultVariantName); 
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
   // weight-only kernels cover every group size / sym of a bit width: listed under the base name
-  static const char* qnames[QT_COUNT] = {"fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16", "w8a16", "w4a4_g128_sym", "w2a16"};
-  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4, 2};
+  static const char* qnames[QT_COUNT] = {"fp16",          "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16",           "w8a16",
+                                         "w4a4_g128_sym", "w2a16",        "w8a8_g-1_sym_E4M3", "bf16"};
+  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4, 2, 8, 16};
   std::string out;
   const auto& vs = variants();
   for (size_t i = 0; i < vs.size(); ++i) {
@@ -732,7 +755,7 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
   int st = check_variant(variant);
   if (st) return st;
   int qt = 0;
-  st = qtype_of(a_bits, w_bits, -1, 1, &qt);
+  st = qtype_of(a_bits, w_bits, -1, 1, MXMOE_GG_FMT_DEFAULT, &qt);
   if (st) return st;
   const TileGeom& g = variants()[variant].geom[qt];
   if (bm) *bm = g.bm;
@@ -914,7 +937,8 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
     hp[i] = HostProblem{h[0 * problem_count + i], h[1 * problem_count + i], h[2 * problem_count + i],
                         h[3 * problem_count + i], h[4 * problem_count + i], (int)h_problem_sizes[i].x,
                         (int)h_problem_sizes[i].y, (int)h_problem_sizes[i].z, h_qbits_list[i].a_bits,
-                        h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0};
+                        h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0,
+                        h_qbits_list[i].fmt};
   // 2. plan with the same NULL / alignment checks as mxmoe_gg_plan (a bad pointer is an error code,
   //    never a fault inside the LDS-DMA kernel)
   int variant;

@@ -32,7 +32,14 @@
 namespace mxmoe {
 
 // QT_I4G: w4a4_g128_sym (A and B int4 with one fp16 scale per 128-K group)
-enum QType : int32_t { QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_I4G = 5, QT_W2A16 = 6, QT_COUNT = 7 };
+// QT_F8: w8a8_g-1_sym_E4M3 (A and B OCP fp8 e4m3, per-channel fp16 scales, f32 accumulate)
+// QT_BF16: bf16 A and B, f32 accumulate, fp16 C
+enum QType : int32_t {
+  QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_I4G = 5, QT_W2A16 = 6, QT_F8 = 7, QT_BF16 = 8,
+  QT_COUNT = 9
+};
+// quant types whose epilogue applies the per-channel scales sa[m] * sb[n]
+constexpr bool qt_scaled(int qt) { return qt == QT_I8 || qt == QT_I4 || qt == QT_F8; }
 
 // One row of the plan table (64 B), written by the host planner into the workspace.
 struct GGMeta {
@@ -87,6 +94,8 @@ typedef int32_t v2i __attribute__((ext_vector_type(2)));
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef int32_t v8i __attribute__((ext_vector_type(8)));
 
 // Compile-time tile geometry. All dtypes stage 128 bytes of K per stage.
 template <int BM_, int BN_, int WM_, int WN_, int MIN_WAVES_PER_EU_>
@@ -141,7 +150,24 @@ template <>
 struct AccT<QT_F16> {
   typedef v4f type;
 };
+template <>
+struct AccT<QT_F8> {
+  typedef v4f type;
+};
+template <>
+struct AccT<QT_BF16> {
+  typedef v4f type;
+};
 
+// fp8 e4m3 x e4m3 over K = 128 (one 128-B v2 stage), f32 accumulate: the block-scaled MFMA with
+// every 32-element block scale = 2^0 (e8m0 code 127), i.e. the plain fp8 dot product at twice the
+// bf16 MFMA rate (MI355X_MICROARCH.md, Matrix cores). Format code 0 = fp8 e4m3 for both operands.
+__device__ __forceinline__ v4f mfma_f8_k128(const v8i& b, const v8i& a, const v4f& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, 0, 0, 0, 127, 0, 127);
+}
+__device__ __forceinline__ v8i cat_v4i(const v4i& lo, const v4i& hi) {
+  return v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
 // One output tile of one problem.
 template <class Cfg, int QT>
 __device__ __forceinline__ void gg_tile(const GGMeta& mt, const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
@@ -429,6 +455,15 @@ __device__ __forceinline__ uint2 scale_pack4(const v4i& acc, _Float16 sa, uint2 
                    (_Float16)mul_f32_f16hi((float)(acc[3] >> SHIFT), s23)};
   return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
 }
+// fp8 path: the accumulator is already f32 (no integer conversion); same scale arithmetic
+__device__ __forceinline__ uint2 scale_pack4f(const v4f& acc, _Float16 sa, uint2 sbw) {
+  const h2_t sa2 = {sa, sa};
+  const uint32_t s01 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw.x));
+  const uint32_t s23 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw.y));
+  const h2_t lo = {(_Float16)mul_f32_f16lo(acc[0], s01), (_Float16)mul_f32_f16hi(acc[1], s01)};
+  const h2_t hi = {(_Float16)mul_f32_f16lo(acc[2], s23), (_Float16)mul_f32_f16hi(acc[3], s23)};
+  return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+}
 __device__ __forceinline__ uint2 pack4_f16(const v4f& acc) {
   const h2_t lo = {(_Float16)acc[0], (_Float16)acc[1]}, hi = {(_Float16)acc[2], (_Float16)acc[3]};
   return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
@@ -586,7 +621,15 @@ struct V2Half {
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[t][j], a[t][i], acc[i][j], 0, 0, 0);
+      } else if constexpr (QT == QT_BF16) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, b[t][j]),
+                                                                __builtin_bit_cast(v8bf, a[t][i]), acc[i][j], 0, 0, 0);
       } else {
+        static_assert(QT == QT_F16, "V2Half: fp8 tiles run the plain v2 mainloop (one K=128 MFMA per stage)");
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -683,7 +726,22 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   auto compute = [&](int buf) {
     const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
     const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
-    if constexpr (QT == QT_I4) {
+    if constexpr (QT == QT_F8) {
+      // one K = 128 MFMA per fragment pair and stage: lane group g holds the 16-B chunks g and g + 4
+      // (the int8 path's two K halves), the same K assignment for A and B
+      const uint32_t off0 = (uint32_t)((g ^ swz) << 4), off1 = (uint32_t)(((4 + g) ^ swz) << 4);
+      v8i b[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j] = cat_v4i(*reinterpret_cast<const v4i*>(Bs + j * 2048 + off0), *reinterpret_cast<const v4i*>(Bs + j * 2048 + off1));
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const v8i a = cat_v4i(*reinterpret_cast<const v4i*>(As + i * 2048 + off0),
+                              *reinterpret_cast<const v4i*>(As + i * 2048 + off1));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_f8_k128(b[j], a, acc[i][j]);
+      }
+    } else if constexpr (QT == QT_I4) {
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
@@ -725,6 +783,17 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
             for (int j = 0; j < FN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+        } else if constexpr (QT == QT_BF16) {
+          v8bf a[FM], b[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v8bf*>(As + i * 2048 + off);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v8bf*>(Bs + j * 2048 + off);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
         } else {
           v8h a[FM], b[FN];
 #pragma unroll
@@ -745,12 +814,12 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   // is issued with stage 0's DMA and written after the prologue barrier, so its latency hides
   // under stage 0's and no register stays live across the mainloop.
   _Float16 sc = 0;
-  if constexpr (QT != QT_F16) {
+  if constexpr (qt_scaled(QT)) {
     if (tid < Cfg::BM) sc = SA[min(m0 + tid, M - 1)];
     else if (tid >= 256) sc = SB[min(n0 + tid - 256, N - 1)];
   }
   auto stash_scale = [&]() {
-    if constexpr (QT != QT_F16) {
+    if constexpr (qt_scaled(QT)) {
       if (tid < Cfg::BM || tid >= 256) reinterpret_cast<_Float16*>(lds + Cfg::LDS_BYTES)[tid] = sc;
     }
   };
@@ -807,7 +876,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       }
     }
     stash_scale();  // the rings are dead: the scale stash (past the epilogue image) is free
-    if constexpr (QT != QT_F16) __syncthreads();
+    if constexpr (qt_scaled(QT)) __syncthreads();
   } else if constexpr ((ABL & V2_STAGGER) != 0) {
     typedef V2Half<Cfg, QT> Half;
     auto hread = [&](Half& f, int buf, int h) {
@@ -875,7 +944,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   // int paths: the tile's row / column scales were staged in LDS during the prologue
   const _Float16* sl = reinterpret_cast<const _Float16*>(lds + Cfg::LDS_BYTES);
   uint2 sbw[FN];
-  if constexpr (QT != QT_F16) {
+  if constexpr (qt_scaled(QT)) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * e_g);
   }
@@ -883,11 +952,12 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   for (int i = 0; i < FM; ++i) {
     const int ml = i * 16 + e_r16;
     _Float16 sai = 0;
-    if constexpr (QT != QT_F16) sai = sl[wm * Cfg::WTM + ml];
+    if constexpr (qt_scaled(QT)) sai = sl[wm * Cfg::WTM + ml];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       uint2 pk;
-      if constexpr (QT == QT_F16) pk = pack4_f16(acc[i][j]);
+      if constexpr (QT == QT_F16 || QT == QT_BF16) pk = pack4_f16(acc[i][j]);
+      else if constexpr (QT == QT_F8) pk = scale_pack4f(acc[i][j], sai, sbw[j]);
       else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
       const int q = 2 * j + (e_g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
@@ -1657,6 +1727,16 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   } else if ((QM & (1 << QT_I4G)) && mt.qtype == QT_I4G) {
     if (cls == 0) gg_tile_g128<V2Cfg<256>>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
     else gg_tile_g128<V2Cfg<128>>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+  } else if ((QM & (1 << QT_F8)) && mt.qtype == QT_F8) {
+    // one K = 128 MFMA per stage: no K halves to stagger, so the plain v2 mainloop (two 64-KiB
+    // stages, inside either LDS image)
+    constexpr int F8ABL = ABL & ~(V2_STAGGER | V2_B3);
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F8, F8ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v2<V2Cfg<128>, QT_F8, F8ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);  // no 64-row class
+  } else if ((QM & (1 << QT_BF16)) && mt.qtype == QT_BF16) {
+    if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_BF16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_BF16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v2<V2Cfg<64>, QT_BF16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);

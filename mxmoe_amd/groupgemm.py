@@ -2,6 +2,8 @@
 
 Reference interface mirrored (SeaCatComplexes/MxMoE):
   * per-problem QParams {qbits=(a_bits, w_bits), gsize, sym} ..... quantize.cuh:14-25
+    (+ the operand format of the reference's fp8 / bf16 strategies: QConfig USE_FP, MMA_E4M3_K32,
+    MMA_BF16_FP32 — tile_config.py:40-106, 192)
   * the host API groupgemm_hz_fused_<i>(ptr_As, ptr_Bs, ptr_scale_a, ptr_scale_b, ptr_Cs, ...,
     problem_sizes, qbits_list, problem_count) ...................... kernel_sketch.py:25-46, 82-145
   * the kernel registry (name -> FuncType), registry.cuh:72-107 .... ``registry()``
@@ -22,18 +24,39 @@ import torch
 from . import _native as nat
 
 
+FMT_CODES = {"": nat.FMT_DEFAULT, "E4M3": nat.FMT_E4M3, "bf16": nat.FMT_BF16}
+
+
 @dataclasses.dataclass(frozen=True)
 class QParams:
-    """Per-problem quantisation parameters (reference QParams, quantize.cuh:14-25)."""
+    """Per-problem quantisation parameters (reference QParams, quantize.cuh:14-25).
+
+    ``fmt``: "" (fp16 / two's-complement integers), "E4M3" (w8a8_g-1_sym_E4M3: OCP fp8 codes) or
+    "bf16" (16-bit bfloat16 operands). The reference's ``_accfp16`` strategies (fp16 MMA with an fp16
+    accumulator, tile_config.py:94-97) run as their f32-accumulating base type: MFMA has no fp16
+    accumulator, and the f32 sum is the more accurate result of the same products."""
 
     a_bits: int = 16
     w_bits: int = 16
     gsize: int = -1
     sym: bool = True
+    fmt: str = ""
+
+    def __post_init__(self):
+        if self.fmt not in FMT_CODES:
+            raise ValueError(f"unknown operand format {self.fmt!r}")
 
     @property
     def is_quant(self) -> bool:
         return self.a_bits < 16 or self.w_bits < 16
+
+    @property
+    def is_fp8(self) -> bool:
+        return self.fmt == "E4M3"
+
+    @property
+    def fmt_code(self) -> int:
+        return FMT_CODES[self.fmt]
 
     @property
     def is_weight_only(self) -> bool:
@@ -43,21 +66,29 @@ class QParams:
     @property
     def qcfg(self) -> str:
         if not self.is_quant:
-            return "fp16"
-        return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}"
+            return "bf16" if self.fmt == "bf16" else "fp16"
+        return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}" + \
+            ("_E4M3" if self.is_fp8 else "")
 
     @staticmethod
     def from_qcfg(qcfg: str) -> "QParams":
-        if qcfg in ("fp16",):
+        """Any SUPPORTED_QCFG string (tile_config.py:40-59); ``_accfp16`` maps to its base type."""
+        if qcfg in ("fp16", "fp16_accfp16"):
             return QParams()
+        if qcfg == "bf16":
+            return QParams(fmt="bf16")
         w = int(qcfg.split("w")[1].split("a")[0])
         a = int(qcfg.split("a")[1].split("_g")[0])
         g = int(qcfg.split("_g")[1].split("_")[0])
-        return QParams(a_bits=a, w_bits=w, gsize=g, sym="asym" not in qcfg)
+        if qcfg.endswith("_bf16"):
+            raise ValueError(f"{qcfg}: weight-only with bf16 activations is not built on MI355X")
+        return QParams(a_bits=a, w_bits=w, gsize=g, sym="asym" not in qcfg, fmt="E4M3" if qcfg.endswith("_E4M3") else "")
 
 
 FP16 = QParams()
+BF16 = QParams(fmt="bf16")
 W8A8 = QParams(8, 8, -1, True)
+W8A8_E4M3 = QParams(8, 8, -1, True, "E4M3")  # w8a8_g-1_sym_E4M3: OCP fp8 operands, f32 accumulate
 W4A4 = QParams(4, 4, -1, True)
 W4A4_G128 = QParams(4, 4, 128, True)  # w4a4_g128_sym: one scale per 128-K group (cta_gemm.cuh:610-772)
 # weight-only (any group size that is -1 or a multiple of 64 dividing K, sym or asym, 2 / 4 / 8 bits)
@@ -67,7 +98,7 @@ W4A16_G128_SYM = QParams(16, 4, 128, True)
 W8A16_ASYM = QParams(16, 8, -1, False)
 W2A16_G128_ASYM = QParams(16, 2, 128, False)
 
-SUPPORTED = {q.qcfg: q for q in (FP16, W8A8, W4A4, W4A4_G128, W4A16_G128_ASYM, W4A16_ASYM, W4A16_G128_SYM, W8A16_ASYM,
+SUPPORTED = {q.qcfg: q for q in (FP16, BF16, W8A8, W8A8_E4M3, W4A4, W4A4_G128, W4A16_G128_ASYM, W4A16_ASYM, W4A16_G128_SYM, W8A16_ASYM,
                                   QParams(16, 4, -1, True), QParams(16, 8, -1, True), QParams(16, 8, 128, True),
                                   QParams(16, 8, 128, False), W2A16_G128_ASYM, QParams(16, 2, -1, False),
                                   QParams(16, 2, -1, True), QParams(16, 2, 128, True))}
@@ -77,7 +108,7 @@ SUPPORTED = {q.qcfg: q for q in (FP16, W8A8, W4A4, W4A4_G128, W4A16_G128_ASYM, W
 class Problem:
     """One GroupGEMM problem  C[M,N] = A[M,K] . B[N,K]^T  on device tensors.
 
-    fp16: A fp16 [M,K], B fp16 [N,K].  quant: A uint8 [M, K*a_bits/8] / B uint8 [N, K*w_bits/8]
+    fp16 / bf16: A [M,K], B [N,K] 16-bit.  quant (incl. E4M3 codes): A uint8 [M, K*a_bits/8] / B uint8 [N, K*w_bits/8]
     in pack_wxax layout, scale_a fp16 [M], scale_b fp16 [N] (w4a4_g128: [K/128][M] and [K/128][N],
     the permute_scale layout).  C fp16 [M, ldc] (ldc >= N).
     """
@@ -102,7 +133,7 @@ class Problem:
         return nat.GGProblemC(
             A=ptr(self.A), B=ptr(self.B), scale_a=ptr(self.scale_a), scale_b=ptr(self.scale_b), C=ptr(self.C),
             M=self.M, N=self.N, K=self.K, a_bits=self.q.a_bits, w_bits=self.q.w_bits, gsize=self.q.gsize,
-            sym=int(self.q.sym), reserved_=0, lda=self.lda, ldb=self.ldb, ldc=self.ldc)
+            sym=int(self.q.sym), fmt=self.q.fmt_code, lda=self.lda, ldb=self.ldb, ldc=self.ldc)
 
     @property
     def flops(self) -> int:
@@ -178,7 +209,8 @@ def groupgemm_reference_abi(ptr_As: torch.Tensor, ptr_Bs: torch.Tensor, ptr_scal
     P = len(h_problem_sizes)
     dims = (nat.MxmoeDim3 * max(P, 1))(*[nat.MxmoeDim3(int(m), int(n), int(k)) for (m, n, k) in h_problem_sizes])
     qps = (nat.MxmoeQParams * max(P, 1))(
-        *[nat.MxmoeQParams(q.a_bits, q.w_bits, q.gsize, int(q.sym), (ctypes.c_uint8 * 3)()) for q in h_qbits_list])
+        *[nat.MxmoeQParams(q.a_bits, q.w_bits, q.gsize, int(q.sym), q.fmt_code, (ctypes.c_uint8 * 2)())
+          for q in h_qbits_list])
     dev_dims = torch.tensor([[m, n, k] for (m, n, k) in h_problem_sizes], dtype=torch.int32, device=ptr_As.device)
     nat.check(nat.lib().groupgemm_mxmoe(
         ptr_As.data_ptr(), ptr_Bs.data_ptr(), ptr_scale_a.data_ptr(), ptr_scale_b.data_ptr(), ptr_Cs.data_ptr(),

@@ -21,7 +21,7 @@ from typing import Optional, Sequence
 import torch
 
 from .groupgemm import GroupGemm, Problem, QParams
-from .quantize import pack_weightonly_mi355x, pack_wxax, quant_rtn_sym, quant_weightonly
+from .quantize import pack_e4m3, pack_weightonly_mi355x, pack_wxax, quant_e4m3, quant_rtn_sym, quant_weightonly
 from .workload import QShape
 
 
@@ -38,12 +38,13 @@ class LayerInputs:
         """Packed A + packed B + fp16 C + fp16 scales."""
         tot = 0
         for s in self.shapes:
-            ab = 16 if s.qcfg == "fp16" else s.a_bits
-            wb = 16 if s.qcfg == "fp16" else s.w_bits
+            plain = s.qcfg in ("fp16", "bf16")
+            ab = 16 if plain else s.a_bits
+            wb = 16 if plain else s.w_bits
             tot += (s.M * s.K * ab + s.N * s.K * wb) // 8 + 2 * s.M * s.N
-            if s.qcfg != "fp16" and ab == 16:  # weight-only: scale (+ zp) per column and group
+            if not plain and ab == 16:  # weight-only: scale (+ zp) per column and group
                 tot += 2 * s.N * (1 if s.gsize == -1 else s.K // s.gsize) * (1 if s.sym else 2)
-            elif s.qcfg != "fp16":
+            elif not plain:
                 tot += 2 * (s.M + s.N) * (1 if s.gsize == -1 else s.K // s.gsize)
         return tot
 
@@ -56,11 +57,18 @@ def build_layer_inputs(shapes: Sequence[QShape], device="cuda", seed: int = 42,
     probs = []
     for s in shapes:
         M, N, K = s.M, s.N, s.K
-        q = QParams(a_bits=s.a_bits, w_bits=s.w_bits, gsize=s.gsize, sym=s.sym)
+        q = QParams(a_bits=s.a_bits, w_bits=s.w_bits, gsize=s.gsize, sym=s.sym, fmt=s.fmt)
         a = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).to(torch.float16)
         b = (torch.rand(N, K, generator=g, device=dev) * 2 - 1).to(torch.float16)
         C = torch.empty(max(M, 1), N, dtype=torch.float16, device=dev)
-        if q.is_weight_only:
+        if q.is_fp8:
+            qa, sa = quant_e4m3(a)
+            qb, sb = quant_e4m3(b)
+            probs.append(Problem(A=pack_e4m3(qa), B=pack_e4m3(qb), C=C, M=M, N=N, K=K, q=q, scale_a=sa, scale_b=sb))
+            del qa, qb
+        elif q.fmt == "bf16":
+            probs.append(Problem(A=a.to(torch.bfloat16), B=b.to(torch.bfloat16), C=C, M=M, N=N, K=K, q=q))
+        elif q.is_weight_only:
             codes, sz = quant_weightonly(b, q.w_bits, q.gsize, q.sym)
             probs.append(Problem(A=a, B=pack_weightonly_mi355x(codes, q.w_bits), C=C, M=M, N=N, K=K, q=q,
                                  scale_b=sz))

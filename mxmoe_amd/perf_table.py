@@ -8,7 +8,9 @@ produces the same schema for the MI355X kernels and restates the cost function:
 
   {qcfg: {key: {"TileConfig(BM=..., ...)": {"first_iter_cost": ms, "inc": ms per tile, "stderr": ms}}}}
 
-* ``qcfg``: every strategy the MI355X kernels implement (``tile_config.MI355X_QCFG``).
+* ``qcfg``: every strategy the MI355X kernels implement (``tile_config.MI355X_QCFG``); the
+  ``_accfp16`` strategies run their base type's kernel, so their entries are copies of the base
+  entries (``ALIASES``, written by ``dump``), and only ``MEASURED_QCFG`` is swept.
 * ``key``: the reference's generator is not in its tree and its key semantics are undocumented
   (bits_solver reads "1" for weight-only and "3" for weight-activation strategies). Here key k is
   the K class K = 1024·k (k = 1..4); every key is present for every qcfg, so the reference's
@@ -30,18 +32,28 @@ from typing import Optional, Sequence
 from .tile_config import MI355X_QCFG, TileConfig, get_info_from_qcfg_str
 
 K_CLASSES = (1, 2, 3, 4)  # key k <-> K = 1024 * k
+ALIASES = {q: q.replace("_accfp16", "") for q in MI355X_QCFG if "_accfp16" in q}
+MEASURED_QCFG = [q for q in MI355X_QCFG if q not in ALIASES]
+
+
+def _fmt(qcfg: str) -> str:
+    from .groupgemm import QParams
+
+    return QParams.from_qcfg(qcfg).fmt
 
 
 def tile_repr(t: TileConfig, qcfg: str) -> str:
     """The reference TileConfig repr (tile_config.py:195-264 dataclass repr, as in performance_table.json)."""
     w, a, g, sym = get_info_from_qcfg_str(qcfg)
 
+    use_fp = qcfg.endswith("_E4M3")  # QCFG_W8A8_E4M3 (tile_config.py:192): USE_FP=True
+
     def qc(bits, gs, sy, dim="K"):
         kind = "NO_QUANT" if bits >= 16 else "QConfig"
         if bits >= 16:
             gs, sy, dim = -1, True, "K"
-        return (f"{kind}(T_PACK='half', QBITS={bits}, GSIZE={gs}, SYM={sy}, PACK_DIM='PackDim::{dim}', USE_FP=False, "
-                f"T_SCALE='half')")
+        return (f"{kind}(T_PACK='half', QBITS={bits}, GSIZE={gs}, SYM={sy}, PACK_DIM='PackDim::{dim}', "
+                f"USE_FP={use_fp and bits < 16}, T_SCALE='half')")
 
     # weight-only B is packed along N (pack_weightonly, quantize.cuh:318-421): PackDim::MN
     return (f"TileConfig(BM={t.BM}, BN={t.BN}, BK={t.BK}, WM={t.WM}, WN={t.WN}, WK={t.WK}, STAGE={t.STAGE}, "
@@ -81,6 +93,9 @@ def runtime_cost(workloads, strategies: Sequence[str], table: dict, tiles: dict)
         row = []
         for w in exp:
             row.append([table[q][k_key(w.K)][tile_repr(tiles[q], q)]["inc"] * num_tiles(w.M, w.N, tiles[q])
+                        if q in table else
+                        table[ALIASES[q]][k_key(w.K)][tile_repr(tiles[ALIASES[q]], ALIASES[q])]["inc"] *
+                        num_tiles(w.M, w.N, tiles[ALIASES[q]])
                         for q in strategies])
         out.append(row)
     return out
@@ -111,11 +126,13 @@ def auto_tiles(qcfgs: Sequence[str] = MI355X_QCFG) -> dict:
             vid = next(v["id"] for v in by_id.values() if v["name"].startswith("v3_256x128"))
         tiles = by_id[vid]["tiles"]
         t = tiles[q if q in tiles else f"w{w}a16"]
-        out[q] = dataclasses.replace(t, MMA="MFMA_F16_F32" if a == 16 else "MFMA_I8_K64")
+        mma = ("MFMA_F8_K128" if q.endswith("_E4M3") else "MFMA_BF16_F32" if q == "bf16" else
+               "MFMA_F16_F32" if a == 16 else "MFMA_I8_K64")
+        out[q] = dataclasses.replace(t, MMA=mma)
     return out
 
 
-def measure(qcfgs: Sequence[str] = MI355X_QCFG, sizes: Sequence[int] = (16, 32, 64, 128, 256), iters: int = 20,
+def measure(qcfgs: Sequence[str] = MEASURED_QCFG, sizes: Sequence[int] = (16, 32, 64, 128, 256), iters: int = 20,
             device: Optional[str] = None, log=None) -> dict:
     """Run the sweep on the current GPU; returns the table (reference schema + the raw points)."""
     import torch
@@ -133,7 +150,8 @@ def measure(qcfgs: Sequence[str] = MI355X_QCFG, sizes: Sequence[int] = (16, 32, 
         for k in K_CLASSES:
             K = 1024 * k
             M, N = 4 * t.BM, 4 * t.BN  # 16 tiles per problem
-            shapes = [QShape(shape=[M, N, K], w_bits=w, a_bits=a, gsize=g, sym=sym) for _ in range(max(sizes))]
+            shapes = [QShape(shape=[M, N, K], w_bits=w, a_bits=a, gsize=g, sym=sym, fmt=_fmt(q))
+                      for _ in range(max(sizes))]
             inp = build_layer_inputs(shapes, device=device or "cuda", seed=k)
             xs, ys = [], []
             for P in sizes:
@@ -151,6 +169,26 @@ def measure(qcfgs: Sequence[str] = MI355X_QCFG, sizes: Sequence[int] = (16, 32, 
     return table
 
 
-def dump(table: dict, path: str) -> None:
+def with_aliases(table: dict) -> dict:
+    """The table plus an entry for every ``_accfp16`` strategy whose base type was measured (the
+    same kernel runs both), keyed by the alias's own TileConfig repr."""
+    out = dict(table)
+    tiles = tiles_from_table(table)
+    for alias, base in ALIASES.items():
+        if base in table:
+            out[alias] = {k: {tile_repr(tiles[base], alias): e for e in v.values()} for k, v in table[base].items()}
+    return out
+
+
+def dump(table: dict, path: str, merge: bool = False) -> None:
+    """Write the table (with alias entries); merge=True keeps the other qcfgs of an existing file."""
+    import os
+
+    if merge and os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+        old.update(table)
+        table = old
+    table = with_aliases({q: v for q, v in table.items() if q not in ALIASES})
     with open(path, "w") as f:
         json.dump(table, f, indent=1)

@@ -87,6 +87,30 @@ def unpack_wxax(p: torch.Tensor, bits: int, K: int) -> torch.Tensor:
     raise ValueError("only support [4, 8] bits")
 
 
+E4M3_MAX = 448.0  # largest finite OCP e4m3 value
+
+
+def quant_e4m3(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-row E4M3 quantisation of fp16 [rows, K] for w8a8_g-1_sym_E4M3 -> (uint8 OCP e4m3 codes in
+    logical K order, fp16 scales [rows]): scale = fp16(amax / 448) (0 -> 1), code = e4m3_rn(f32(x) /
+    f32(scale)), saturating. The reference defines the strategy (QCFG_W8A8_E4M3, tile_config.py:192)
+    but ships no quantiser for it; this is the natural per-channel analogue of quant_weight
+    (quantize.cuh:218-279), restated in oracle/gg_oracle.c (oracle_quant_e4m3)."""
+    if x.dtype != torch.float16:
+        raise TypeError("quant_e4m3 expects fp16 input")
+    amax = x.abs().amax(dim=-1).float()
+    scale = (amax / E4M3_MAX).half()
+    scale = torch.where(scale == 0, torch.ones_like(scale), scale)
+    q = (x.float() / scale.float()[:, None]).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), scale
+
+
+def pack_e4m3(codes: torch.Tensor) -> torch.Tensor:
+    """uint8 e4m3 codes [rows, K] -> the pack_wxax 8-bit byte order (QCFG_W8A8_E4M3: T_PACK half,
+    PACK_DIM K — each 16-bit word holds elements (2j, 2j+1) with 2j in the high byte)."""
+    return pack_wxax(codes.view(torch.int8), 8)
+
+
 def quantize_pack(x: torch.Tensor, bits: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """fp16 [rows, K] -> (packed uint8, fp16 scale, int8 codes)."""
     q, s = quant_rtn_sym(x, bits)

@@ -29,13 +29,16 @@ SUPPORTED_QCFG = [
       for ty in ["", "_accfp16", "_bf16"]],
 ]
 
-# what the MI355X kernels implement (bf16 / fp8 and the _accfp16 forms are not built)
-MI355X_QCFG = ["fp16", "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a4_g128_sym",
-               *[f"w{w}a16_g{g}_{s}" for w in (4, 8, 2) for g in (-1, 128) for s in ("sym", "asym")]]
+# what the MI355X kernels implement; the _accfp16 forms run as their f32-accumulating base type
+# (MFMA has no fp16 accumulator); the weight-only _bf16 forms are not built
+MI355X_QCFG = ["fp16", "fp16_accfp16", "bf16", "w8a8_g-1_sym", "w8a8_g-1_sym_E4M3", "w4a4_g-1_sym", "w4a4_g128_sym",
+               *[f"w{w}a16_g{g}_{s}{t}" for w in (4, 8, 2) for g in (-1, 128) for s in ("sym", "asym")
+                 for t in ("", "_accfp16")]]
 
 
 def get_info_from_qcfg_str(qcfg: str) -> tuple[int, int, int, bool]:
-    """(w_bits, a_bits, gsize, sym) from "w8a8_g-1_sym" (tile_config.py:288-294)."""
+    """(w_bits, a_bits, gsize, sym) from "w8a8_g-1_sym" (tile_config.py:288-294); format suffixes
+    (``_E4M3``, ``_accfp16``, ``_bf16``) do not change the bit widths."""
     if qcfg in ("fp16", "fp16_accfp16", "bf16"):
         return 16, 16, -1, True
     splits = qcfg.split("_")
@@ -139,7 +142,9 @@ def variant_key(qcfg: str) -> str:
     """The key a variant lists a qcfg under: weight-only strategies by their base name
     (``w4a16_g128_asym`` -> ``w4a16``: one tile body serves every group size / symmetry);
     wxax and fp16 strategies by their full name (``w4a4_g128_sym`` is its own body)."""
-    m = re.match(r"^(w\d+a16)_g-?\d+_a?sym$", qcfg)
+    if qcfg == "fp16_accfp16":
+        return "fp16"
+    m = re.match(r"^(w\d+a16)_g-?\d+_a?sym(_accfp16)?$", qcfg)
     return m.group(1) if m else qcfg
 
 

@@ -50,6 +50,7 @@ class QShape:
     a_bits: int = 16
     gsize: int = -1
     sym: bool = True
+    fmt: str = ""  # "" | "E4M3" | "bf16" (written to JSON only when set: reference files are unchanged)
 
     @property
     def M(self) -> int:
@@ -66,31 +67,44 @@ class QShape:
     @property
     def qcfg(self) -> str:
         if self.w_bits == 16 and self.a_bits == 16:
-            return "fp16"
-        return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}"
+            return "bf16" if self.fmt == "bf16" else "fp16"
+        return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}" + \
+            ("_E4M3" if self.fmt == "E4M3" else "")
 
     @property
     def flops(self) -> int:
         return 2 * self.M * self.N * self.K
 
     def to_json(self) -> dict:
-        return {"shape": list(self.shape), "w_bits": self.w_bits, "a_bits": self.a_bits, "gsize": self.gsize,
-                "sym": self.sym}
+        d = {"shape": list(self.shape), "w_bits": self.w_bits, "a_bits": self.a_bits, "gsize": self.gsize,
+             "sym": self.sym}
+        if self.fmt:
+            d["fmt"] = self.fmt
+        return d
 
     @staticmethod
     def from_json(j: dict) -> "QShape":
         return QShape(shape=[int(x) for x in j["shape"]], w_bits=int(j["w_bits"]), a_bits=int(j["a_bits"]),
-                      gsize=int(j["gsize"]), sym=bool(j["sym"]))
+                      gsize=int(j["gsize"]), sym=bool(j["sym"]), fmt=str(j.get("fmt", "")))
 
 
 def parse_qstr(qstr: str) -> dict:
-    """gen_workload.py:51-57."""
-    return {
+    """gen_workload.py:51-57; also the SUPPORTED_QCFG forms that reference parser cannot read
+    (``bf16``, ``fp16[_accfp16]``, ``..._E4M3``; ``_accfp16`` runs as its f32-accumulating base)."""
+    if qstr in ("fp16", "fp16_accfp16", "bf16"):
+        d = dict(FP16_QCFG)
+        if qstr == "bf16":
+            d["fmt"] = "bf16"
+        return d
+    d = {
         "w_bits": int(qstr.split("w")[1].split("a")[0]),
         "a_bits": int(qstr.split("a")[1].split("_g")[0]),
         "gsize": int(qstr.split("_g")[1].split("_")[0]),
         "sym": "asym" not in qstr,
     }
+    if qstr.endswith("_E4M3"):
+        d["fmt"] = "E4M3"
+    return d
 
 
 FP16_QCFG = {"w_bits": 16, "a_bits": 16, "gsize": -1, "sym": True}
@@ -191,14 +205,27 @@ def qwen2_layer11_workload(bs: int = 8192, qconfig: Optional[dict] = None, qstr:
     return generate_workload_from_trace(qwen2_layer11_trace(), bs, 11, qconfig=qconfig, qstr=qstr)
 
 
-def ds2_trace(bs: int = 8192, seed: int = 0) -> dict:
-    """DeepSeek-V2-Lite routing: M_e ~ multinomial(bs*6, dirichlet(20*1_64)) (SURVEY.md §8d)."""
-    s = MODEL_SHAPES["ds2"]
+def synthetic_trace(model: str, bs: int = 8192, seed: int = 0, layer: int = 1) -> dict:
+    """Seeded routing for a model the reference ships no gate trace for (only qwen2_moe's histogram is
+    in the tree): M_e ~ multinomial(bs*topk, dirichlet(20*1_E)), the model's MoE
+    geometry from MODEL_SHAPES (gen_workload.py:16-21 model ids; moe_tracer.py:42-56)."""
+    s = MODEL_SHAPES[model]
     rng = np.random.default_rng(seed)
     p = rng.dirichlet(20.0 * np.ones(s["E"]))
     m = rng.multinomial(bs * s["topk"], p)
     return {"topk": s["topk"], "NK": [s["N"], s["K"]], "num_shared_experts": s["S"],
-            "layer-1": {"access_freq": [int(x) for x in m]}}
+            f"layer-{layer}": {"access_freq": [int(x) for x in m]}}
+
+
+def ds2_trace(bs: int = 8192, seed: int = 0) -> dict:
+    """DeepSeek-V2-Lite routing: M_e ~ multinomial(bs*6, dirichlet(20*1_64)) (SURVEY.md §8d)."""
+    return synthetic_trace("ds2", bs, seed, layer=1)
+
+
+def model_workload(model: str, bs: int = 8192, qconfig: Optional[dict] = None, qstr: Optional[str] = None,
+                   seed: int = 0) -> dict:
+    """One layer ("layer-1") of a model with seeded synthetic routing (mixtral, qwen2_moe_57b, ds2)."""
+    return generate_workload_from_trace(synthetic_trace(model, bs, seed, layer=1), bs, 1, qconfig=qconfig, qstr=qstr)
 
 
 def ds2_workload(bs: int = 8192, qconfig: Optional[dict] = None, qstr: Optional[str] = None, seed: int = 0) -> dict:

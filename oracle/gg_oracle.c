@@ -13,6 +13,14 @@
  *   w4a4 g128     per-group int32 dot products folded with fmaf ... cta_gemm.cuh:610-772
  *   fp16          C = fp16_rn(sum_k a*b) with an f64 accumulator (the reference accumulates in
  *                 f32 on tensor cores, order unspecified: cta_gemm.cuh:7-107) — tolerance-checked.
+ *   bf16          the same with bfloat16 operands (MMA_BF16_FP32, tile_config.py:64-102).
+ *   w8a8 E4M3     OCP fp8 e4m3 operands (QCFG_W8A8_E4M3 tile_config.py:192: T_PACK half, PACK_DIM K,
+ *                 i.e. pack_wxax byte order; mma m16n8k32 e4m3 -> f32, cuda_utils.cuh:385-410), the
+ *                 products exact and summed exactly here (f64), then the wxax epilogue on f32(acc)
+ *                 (mm_tile.cuh:469-496). The reference ships no E4M3 quantiser and no codegen branch
+ *                 for it (compose_kernel.py:47-57): the quantiser below (per-row scale amax/448,
+ *                 one RNE rounding to e4m3, saturating) is this repo's definition — parity unpinned
+ *                 by the reference; the code <-> value map is pinned to torch.float8_e4m3fn in tests.
  * The column-scale index uses the INTENDED sb[n] (SURVEY.md §8(a) a11 documents the reference's
  * lane%4 indexing bug; tests/golden also holds the bug-compatible permuted-scale variant).
  */
@@ -230,6 +238,105 @@ int oracle_gg_quant_grouped(const uint8_t* A, const uint8_t* B, const uint16_t* 
     free(aq);
   }
   free(bq);
+  return rc;
+}
+
+/* ---- OCP fp8 e4m3 (e4m3fn: bias 7, no infinities, S.1111.111 = NaN, max 448) ---- */
+float oracle_e4m3_to_f32(uint8_t v) {
+  const int e = (v >> 3) & 15, m = v & 7;
+  float mag;
+  if (e == 15 && m == 7) return (v & 0x80) ? -NAN : NAN;
+  if (e == 0) mag = ldexpf((float)m, -9); /* subnormal: m * 2^-3 * 2^-6 */
+  else mag = ldexpf(1.0f + (float)m / 8.0f, e - 7);
+  return (v & 0x80) ? -mag : mag;
+}
+
+/* f32 -> e4m3, round to nearest even, saturating to +-448 (NaN -> NaN) */
+uint8_t oracle_f32_to_e4m3(float f) {
+  if (f != f) return 0x7f;
+  const uint8_t sign = signbit(f) ? 0x80 : 0;
+  float a = fabsf(f);
+  if (a >= 448.0f) return sign | 0x7e;
+  /* candidates: every non-negative finite code is monotone in its value; pick the nearest, ties even */
+  int lo = 0, hi = 0x7e;
+  while (hi - lo > 1) { /* largest code with value <= a */
+    const int mid = (lo + hi) / 2;
+    if (oracle_e4m3_to_f32((uint8_t)mid) <= a) lo = mid;
+    else hi = mid;
+  }
+  if (oracle_e4m3_to_f32((uint8_t)hi) <= a) lo = hi;
+  if (lo == 0x7e) return sign | 0x7e;
+  const float vlo = oracle_e4m3_to_f32((uint8_t)lo), vhi = oracle_e4m3_to_f32((uint8_t)(lo + 1));
+  const double dlo = (double)a - vlo, dhi = (double)vhi - a;
+  int q = lo;
+  if (dhi < dlo || (dhi == dlo && (lo & 1))) q = lo + 1;
+  return sign | (uint8_t)q;
+}
+
+/* per-row E4M3 quantisation of fp16 x: scale = fp16(amax / 448) (0 -> 1), q = e4m3_rn(f32(x) / f32(scale)) */
+int oracle_quant_e4m3(const uint16_t* x, uint8_t* q, uint16_t* scale, int64_t rows, int64_t K) {
+  for (int64_t r = 0; r < rows; ++r) {
+    float mx = 0.0f;
+    for (int64_t k = 0; k < K; ++k) {
+      float v = fabsf(oracle_f16_to_f32(x[r * K + k]));
+      if (v > mx) mx = v;
+    }
+    uint16_t s = oracle_f32_to_f16(mx / 448.0f);
+    if ((s & 0x7fff) == 0) s = 0x3c00;
+    scale[r] = s;
+    const float sf = oracle_f16_to_f32(s);
+    for (int64_t k = 0; k < K; ++k) q[r * K + k] = oracle_f32_to_e4m3(oracle_f16_to_f32(x[r * K + k]) / sf);
+  }
+  return 0;
+}
+
+/* ---- w8a8 E4M3 GroupGEMM problem: A [M][lda_b], B [N][ldb_b] bytes in pack_wxax byte order
+ *      (byte 2j holds element 2j+1 and vice versa; the same order on A and B, so the byte-wise dot
+ *      product is the element-wise one). acc = f32(exact sum), C = fp16_rn(0 + acc * f32(fp16_rn(sa*sb))). */
+int oracle_gg_e4m3(const uint8_t* A, const uint8_t* B, const uint16_t* sa, const uint16_t* sb, uint16_t* C,
+                   int64_t M, int64_t N, int64_t K, int64_t lda_b, int64_t ldb_b, int64_t ldc, int nthreads) {
+  float lut[256];
+  for (int i = 0; i < 256; ++i) lut[i] = oracle_e4m3_to_f32((uint8_t)i);
+  int rc = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t m = 0; m < M; ++m) {
+    for (int64_t n = 0; n < N; ++n) {
+      const uint8_t* a = A + m * lda_b;
+      const uint8_t* b = B + n * ldb_b;
+      double acc = 0.0; /* products of e4m3 values have <= 8 significant bits: exact in f64 */
+      for (int64_t k = 0; k < K; ++k) acc += (double)lut[a[k]] * (double)lut[b[k]];
+      const uint16_t s16 = f16_mul(sa[m], sb[n]);
+      const float v = 0.0f + (float)acc * oracle_f16_to_f32(s16);
+      C[m * ldc + n] = oracle_f32_to_f16(v);
+    }
+  }
+  return rc;
+}
+
+/* ---- bf16 GroupGEMM problem (f64 accumulate, RN to fp16). A [M][lda], B [N][ldb] in elements. ---- */
+int oracle_gg_bf16(const uint16_t* A, const uint16_t* B, uint16_t* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                   int64_t ldb, int64_t ldc, int nthreads) {
+  int rc = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t m = 0; m < M; ++m) {
+    for (int64_t n = 0; n < N; ++n) {
+      double acc = 0.0;
+      for (int64_t k = 0; k < K; ++k) {
+        uint32_t ab = (uint32_t)A[m * lda + k] << 16, bb = (uint32_t)B[n * ldb + k] << 16;
+        float af, bf;
+        memcpy(&af, &ab, 4);
+        memcpy(&bf, &bb, 4);
+        acc += (double)af * (double)bf;
+      }
+      C[m * ldc + n] = oracle_f32_to_f16((float)acc);
+    }
+  }
   return rc;
 }
 

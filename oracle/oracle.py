@@ -9,6 +9,11 @@ Every function restates reference arithmetic (SeaCatComplexes/MxMoE):
   gg_quant ............ cta_gemm.cuh:423-608 + mm_tile.cuh:469-496, 610-662
   gg_quant_grouped .... cta_gemm.cuh:610-772 (w4a4 g128: per-group int32 dot products, fmaf fold)
   gg_f16 .............. cta_gemm.cuh:7-107 (f64 accumulate here; tolerance-checked)
+  gg_bf16 ............. the same with bfloat16 operands (MMA_BF16_FP32, tile_config.py:64-102)
+  quant_e4m3 / gg_e4m3 . w8a8_g-1_sym_E4M3 (tile_config.py:45, 192; cuda_utils.cuh:385-410): the
+                         reference has no E4M3 quantiser or codegen branch, so the quantiser is this
+                         repo's definition (parity unpinned by the reference; e4m3 codes pinned to
+                         torch.float8_e4m3fn)
 """
 from __future__ import annotations
 
@@ -51,6 +56,15 @@ def lib() -> ctypes.CDLL:
                                                  c.c_int64, c.c_int64, c.c_int64, c.c_int]
         _lib.oracle_gg_f16.argtypes = [P, P, P, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64,
                                        c.c_int]
+        _lib.oracle_e4m3_to_f32.restype = c.c_float
+        _lib.oracle_e4m3_to_f32.argtypes = [c.c_uint8]
+        _lib.oracle_f32_to_e4m3.restype = c.c_uint8
+        _lib.oracle_f32_to_e4m3.argtypes = [c.c_float]
+        _lib.oracle_quant_e4m3.argtypes = [P, P, P, c.c_int64, c.c_int64]
+        _lib.oracle_gg_e4m3.argtypes = [P, P, P, P, P, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64,
+                                        c.c_int64, c.c_int]
+        _lib.oracle_gg_bf16.argtypes = [P, P, P, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64, c.c_int64,
+                                        c.c_int]
         _lib.oracle_max_threads.restype = c.c_int
     return _lib
 
@@ -134,6 +148,47 @@ def gg_f16(A: np.ndarray, B: np.ndarray, M: int, N: int, K: int, threads: int = 
     B = np.ascontiguousarray(B, np.float16)
     C = np.zeros((M, N), np.float16)
     _chk(lib().oracle_gg_f16(_p(A), _p(B), _p(C), M, N, K, K, K, N, threads), "gg_f16")
+    return C
+
+
+def quant_e4m3(x_f16: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Per-row E4M3: (uint8 e4m3 codes [rows, K] in logical order, fp16 scales [rows])."""
+    x = np.ascontiguousarray(x_f16, dtype=np.float16)
+    rows, K = x.shape
+    q = np.empty((rows, K), np.uint8)
+    s = np.empty((rows,), np.float16)
+    _chk(lib().oracle_quant_e4m3(_p(x), _p(q), _p(s), rows, K), "quant_e4m3")
+    return q, s
+
+
+def e4m3_to_f32(codes: np.ndarray) -> np.ndarray:
+    lut = np.array([lib().oracle_e4m3_to_f32(i) for i in range(256)], np.float32)
+    return lut[np.asarray(codes, np.uint8)]
+
+
+def f32_to_e4m3(x: np.ndarray) -> np.ndarray:
+    f = lib().oracle_f32_to_e4m3
+    return np.array([f(float(v)) for v in np.asarray(x, np.float32).ravel()], np.uint8).reshape(np.shape(x))
+
+
+def gg_e4m3(A: np.ndarray, B: np.ndarray, sa: np.ndarray, sb: np.ndarray, M: int, N: int, K: int,
+            threads: int = 0) -> np.ndarray:
+    """Expected fp16 C [M,N] of one w8a8 E4M3 problem from A [M,K], B [N,K] code bytes (pack_wxax order)."""
+    A = np.ascontiguousarray(A, np.uint8)
+    B = np.ascontiguousarray(B, np.uint8)
+    sa = np.ascontiguousarray(sa, np.float16)
+    sb = np.ascontiguousarray(sb, np.float16)
+    C = np.zeros((M, N), np.float16)
+    _chk(lib().oracle_gg_e4m3(_p(A), _p(B), _p(sa), _p(sb), _p(C), M, N, K, K, K, N, threads), "gg_e4m3")
+    return C
+
+
+def gg_bf16(A: np.ndarray, B: np.ndarray, M: int, N: int, K: int, threads: int = 0) -> np.ndarray:
+    """Expected fp16 C [M,N] of one bf16 problem; A [M,K], B [N,K] as uint16 bfloat16 bit patterns."""
+    A = np.ascontiguousarray(A, np.uint16)
+    B = np.ascontiguousarray(B, np.uint16)
+    C = np.zeros((M, N), np.float16)
+    _chk(lib().oracle_gg_bf16(_p(A), _p(B), _p(C), M, N, K, K, K, N, threads), "gg_bf16")
     return C
 
 

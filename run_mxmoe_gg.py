@@ -15,7 +15,7 @@ and the bench runs in-process on the GPU.
 
 Gate traces: --trace PATH, else calib/gate/{model}/{dataset}/4096/moe-gate.json (gen_workload.py:23-31)
 if present, else the committed qwen2_moe bs=8192 histogram for qwen2_moe / a seeded
-synthetic trace for ds2.
+synthetic trace (workload.synthetic_trace) for ds2, qwen2_moe_57b and mixtral.
 """
 from __future__ import annotations
 
@@ -28,8 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mxmoe_amd.qconfig import get_qcfg_list, load_qconfig  # noqa: E402
-from mxmoe_amd.workload import (MODEL_ID_TO_LAYERS, ds2_trace, generate_workload_from_trace,  # noqa: E402
-                                load_workload, qwen2_hist, qwen2_layer11_trace, save_workload)
+from mxmoe_amd.workload import (MODEL_ID_TO_LAYERS, generate_workload_from_trace, load_workload,  # noqa: E402
+                                qwen2_hist, qwen2_layer11_trace, save_workload, synthetic_trace)
 
 CUR_DIR = ROOT
 
@@ -48,8 +48,8 @@ def find_trace(model: str, dataset: str, layer: int, explicit: str | None) -> di
         for li in range(MODEL_ID_TO_LAYERS[model]):  # the only routing data in the reference (§8d)
             t[f"layer-{li}"] = h
         return t
-    if model == "ds2":
-        t = ds2_trace()
+    if model in ("ds2", "qwen2_moe_57b", "mixtral"):
+        t = synthetic_trace(model)
         h = t.pop("layer-1")
         for li in range(MODEL_ID_TO_LAYERS[model]):
             t[f"layer-{li}"] = h

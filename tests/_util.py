@@ -5,11 +5,18 @@ import numpy as np
 import torch
 
 from mxmoe_amd import _native as nat
-from mxmoe_amd.groupgemm import FP16, W4A4, W4A4_G128, W8A8, Problem, QParams
-from mxmoe_amd.quantize import pack_wxax, quant_rtn_sym
+from mxmoe_amd.groupgemm import BF16, FP16, W4A4, W4A4_G128, W8A8, W8A8_E4M3, Problem, QParams
+from mxmoe_amd.quantize import pack_e4m3, pack_wxax, quant_e4m3, quant_rtn_sym
 from oracle import oracle, weightonly
 
-QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4, "w4a4_g128_sym": W4A4_G128}
+QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4, "w4a4_g128_sym": W4A4_G128,
+         "w8a8_g-1_sym_E4M3": W8A8_E4M3, "bf16": BF16}
+
+
+def exact_compare(q: QParams) -> bool:
+    """Integer-accumulating quant types are checked bit for bit; fp16 / bf16 / weight-only / E4M3
+    (f32 sums in an unspecified order) within the fp16 tolerance."""
+    return q.is_quant and not q.is_weight_only and not q.is_fp8
 
 
 class HostProblem:
@@ -21,7 +28,17 @@ class HostProblem:
         self.M, self.N, self.K, self.q = M, N, K, q
         a = (torch.rand(M, K, generator=g, dtype=torch.float32) * 2 - 1).to(torch.float16)
         b = (torch.rand(N, K, generator=g, dtype=torch.float32) * 2 - 1).to(torch.float16)
-        if q.is_weight_only:
+        if q.is_fp8:
+            qa, sa = quant_e4m3(a)
+            qb, sb = quant_e4m3(b)
+            self.qa, self.qb = qa.numpy(), qb.numpy()
+            self.A, self.B = pack_e4m3(qa).numpy(), pack_e4m3(qb).numpy()
+            self.sa, self.sb = sa.numpy(), sb.numpy()
+        elif q.fmt == "bf16":
+            self.A = a.to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+            self.B = b.to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+            self.sa = self.sb = None
+        elif q.is_weight_only:
             # oracle quantisation; B either packed straight into the kernel layout or built in the
             # reference's packed format and converted by the library (the drop-in route)
             qv, sz = weightonly.quant_wo(b.numpy(), q.w_bits, q.gsize, q.sym)
@@ -53,13 +70,22 @@ class HostProblem:
             self.Cbuf = C
             Cview = C[:, c_col0:]
         self.c_col0 = c_col0
+        if q.fmt == "bf16":
+            tA = torch.from_numpy(self.A.view(np.int16)).view(torch.bfloat16).to(dev)
+            tB = torch.from_numpy(self.B.view(np.int16)).view(torch.bfloat16).to(dev)
+        else:
+            tA, tB = torch.from_numpy(self.A).to(dev), torch.from_numpy(self.B).to(dev)
         self.problem = Problem(
-            A=torch.from_numpy(self.A).to(dev), B=torch.from_numpy(self.B).to(dev), C=Cview, M=M, N=N, K=K, q=q,
+            A=tA, B=tB, C=Cview, M=M, N=N, K=K, q=q,
             scale_a=None if self.sa is None else torch.from_numpy(self.sa).to(dev),
             scale_b=None if self.sb is None else torch.from_numpy(self.sb).to(dev),
             ldc=self.ldc if C is None else C.shape[1])
 
     def expected(self) -> np.ndarray:
+        if self.q.is_fp8:
+            return oracle.gg_e4m3(self.A, self.B, self.sa, self.sb, self.M, self.N, self.K)
+        if self.q.fmt == "bf16":
+            return oracle.gg_bf16(self.A, self.B, self.M, self.N, self.K)
         if self.q.is_weight_only:
             q = self.q
             return weightonly.gemm(self.A, weightonly.dequant(self.qb, self.sb, self.N, self.K, q.w_bits, q.gsize, q.sym))

@@ -46,7 +46,8 @@ def test_cli_check_mixed_qconfig_with_exporter_tile_config(out_dir):
     assert (out_dir / "out" / "workloads" / "qwen2_moe-wiki2-512-5.0_lp1.json").exists()
 
 
-@pytest.mark.parametrize("qstr", ["w4a16_g128_asym", "w4a4_g128_sym", "w8a16_g-1_sym"])
+@pytest.mark.parametrize("qstr", ["w4a16_g128_asym", "w4a4_g128_sym", "w8a16_g-1_sym", "w8a8_g-1_sym_E4M3", "bf16",
+                                  "fp16_accfp16"])
 def test_cli_check_qstr(out_dir, qstr):
     res = run_mxmoe_gg.main(["--bs", "512", "--layer", "11", "--qstr", qstr, "--mode", "check", "--iters", "3"])
     vs = res["variants"][11]

@@ -13,7 +13,7 @@ import torch
 
 from mxmoe_amd import _native as nat
 from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, GroupGemm, Problem, QParams, group_gemm, groupgemm_reference_abi
-from tests._util import HostProblem, assert_f16_close
+from tests._util import HostProblem, assert_f16_close, exact_compare
 
 pytestmark = pytest.mark.gpu
 
@@ -23,7 +23,7 @@ DEV = "cuda"
 def _check(hps):
     for hp in hps:
         out, ref = hp.result(), hp.expected()
-        if hp.q.is_quant and not hp.q.is_weight_only:  # int32 accumulation: bit-exact
+        if exact_compare(hp.q):  # int32 accumulation: bit-exact
             mism = np.count_nonzero(out.view(np.uint16) != ref.view(np.uint16))
             assert mism == 0, f"{hp.q.qcfg} M={hp.M} N={hp.N} K={hp.K}: {mism} mismatching outputs"
         else:

@@ -157,3 +157,24 @@ def test_cpu_plumbing_bs128_config0(tmp_path, monkeypatch):
     tot = sum(h)
     assert [p["shape"][0] for p in gate_up[:-1]] == [int(m / tot * 128 * 4) for m in h]
     assert (tmp_path / "out" / "bench" / "qwen2_moe-wiki2-128-fp16-layer-11-gate_up-cpu.csv").exists()
+
+
+def test_other_model_workloads_follow_gen_workload_rules():
+    """mixtral / qwen2_moe_57b (gen_workload.py:16-21; MODEL_SHAPES) with seeded synthetic routing:
+    routed M_e = int(p_e * T * topk), shared expert last (none for mixtral), gate_up N = 2 * N_e."""
+    from mxmoe_amd.workload import MODEL_SHAPES, load_workload, model_workload, synthetic_trace
+
+    for model in ("mixtral", "qwen2_moe_57b"):
+        s = MODEL_SHAPES[model]
+        wl = load_workload(model_workload(model, 4096, qstr="w8a8_g-1_sym_E4M3"))["layer-1"]
+        t = synthetic_trace(model, 4096)
+        freq = t["layer-1"]["access_freq"]
+        assert sum(freq) == 4096 * s["topk"]
+        n_shared = 1 if s["S"] else 0
+        assert len(wl["gate_up"]) == s["E"] + n_shared and len(wl["down"]) == s["E"] + n_shared
+        for e, p in enumerate(wl["gate_up"][: s["E"]]):
+            assert p.shape == [int(freq[e] / sum(freq) * 4096 * s["topk"]), 2 * s["N"], s["K"]]
+            assert p.qcfg == "w8a8_g-1_sym_E4M3"
+        if n_shared:
+            assert wl["gate_up"][-1].shape == [4096, int(2 * s["N"] * s["S"]), s["K"]]
+            assert wl["down"][-1].shape == [4096, s["K"], int(s["N"] * s["S"])]

@@ -12,18 +12,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from mxmoe_amd import perf_table  # noqa: E402
-from mxmoe_amd.tile_config import MI355X_QCFG  # noqa: E402
+from mxmoe_amd.perf_table import MEASURED_QCFG  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "mxmoe_amd", "workloads", "performance_table_mi355x.json"))
-    ap.add_argument("--qcfgs", default=",".join(MI355X_QCFG))
+    ap.add_argument("--qcfgs", default=",".join(MEASURED_QCFG))
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--merge", action="store_true", help="keep the other qcfgs of an existing --out file")
     args = ap.parse_args()
     table = perf_table.measure([q for q in args.qcfgs.split(",") if q], iters=args.iters,
                                log=lambda m: print(m, file=sys.stderr, flush=True))
-    perf_table.dump(table, args.out)
+    perf_table.dump(table, args.out, merge=args.merge)
     print(args.out)
 
 
