@@ -64,7 +64,6 @@ struct Variant {
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
   int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
   void (*launch)(const GGArgs&, int grid, int qmask, hipStream_t);  // qmask: 1 << QType present
-  bool persistent = false;  // one workgroup per CU popping the per-XCD tile queues (no split-K)
 };
 
 template <class C16, class C8, class C4>
@@ -105,35 +104,6 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
         else launch_v2_q<0, 63>(a, grid, s);
         break;
     }
-  }
-}
-
-// persistent v2: grid = one workgroup per CU (at most one per tile)
-int device_cus() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cus[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
-template <int ABL, int QM>
-void launch_v2p_q(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gg_v2p_kernel<ABL, QM>), dim3(grid), dim3(512), 0, s, a);
-}
-template <int ABL>
-void launch_v2p(const GGArgs& a, int grid, int qmask, hipStream_t s) {
-  const int g = std::max(1, std::min(grid, device_cus()));
-  switch (qmask & 511) {
-    case 1: launch_v2p_q<ABL, 1>(a, g, s); break;
-    case 2: launch_v2p_q<ABL, 2>(a, g, s); break;
-    case 4: launch_v2p_q<ABL, 4>(a, g, s); break;
-    case 6: launch_v2p_q<ABL, 6>(a, g, s); break;  // w8a8 + w4a4 (mixed-precision layers)
-    case 256: launch_v2p_q<ABL, 256>(a, g, s); break;
-    default: launch_v2p_q<ABL, 263>(a, g, s); break;  // fp16 / w8a8 / w4a4 / bf16 mixes
   }
 }
 
@@ -185,24 +155,6 @@ Variant make_v3(const char* name) {
   v.k_stage_bytes = 0;
   v.tail_bm = 128;
   v.launch = &launch_v3<BN, WN, NBUF, DIST>;
-  return v;
-}
-
-template <int ABL>
-Variant make_v2p(const char* name) {
-  Variant v;
-  v.name = name;
-  v.kind = Kind::V2;
-  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {0, 0, 0, 0};
-  for (int q : {QT_F16, QT_I8, QT_I4, QT_BF16}) v.geom[q] = {256, 256, 128, 512};
-  v.threads = 512;
-  v.lds_bytes = V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA;
-  v.chunk = 32;
-  v.k_stage_bytes = 0;
-  v.tail_bm = 128;
-  v.tail2_bm = 0;
-  v.launch = &launch_v2p<ABL>;
-  v.persistent = true;
   return v;
 }
 
@@ -259,8 +211,6 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | ABL_WO_BTILED>("abl_v2s_wo_btiled"),
       make_v2<V2_STAGGER | ABL_WO_NODMA>("abl_v2s_wo_nodma"),
       make_v2<V2_STAGGER | ABL_WO_NOCOMPUTE>("abl_v2s_wo_nocompute"),
-      // persistent staggered v2: next tile's prologue under the current epilogue, direct stores
-      make_v2p<V2_STAGGER>("v2p_256x256_w8_dma_stagger_persistent"),
   };
   return v;
 }
@@ -339,24 +289,19 @@ struct HostProblem {
 };
 
 // Workspace: [GGMeta x P][ptr_A x P][ptr_B x P][ptr_SA x P][ptr_SB x P][ptr_C x P][TileDesc x grid]
-// workspace: plan table | 5 pointer columns | tile table | persistent queue words (heads and done
-// zero between launches, per-XCD lengths) | split-K counters (one per tile slot, zero between
-// launches) | persistent store sink | split-K slabs. Everything before the sink is uploaded.
+// workspace: plan table | 5 pointer columns | tile table | split-K counters (one per tile slot,
+// zero between launches) | split-K slabs
 struct WsLayout {
-  size_t meta, ptr, tiles, pdesc, pq, counters, trash, slabs, total;
-  size_t image() const { return meta + 5 * ptr + tiles + pdesc + pq + counters; }
+  size_t meta, ptr, tiles, counters, slabs, total;
 };
-WsLayout ws_layout(int P, int grid, int slabs, bool persistent = false) {
+WsLayout ws_layout(int P, int grid, int slabs) {
   WsLayout l;
   l.meta = align_up((size_t)std::max(P, 1) * sizeof(GGMeta), 256);
   l.ptr = align_up((size_t)std::max(P, 1) * sizeof(void*), 256);
   l.tiles = align_up((size_t)std::max(grid, 1) * sizeof(TileDesc), 256);
-  l.pdesc = persistent ? (size_t)std::max(grid, 1) * sizeof(PTileDesc) : 0;
-  l.pq = PQ_BYTES;
   l.counters = slabs ? align_up((size_t)grid * sizeof(int32_t), 256) : 0;
-  l.trash = PQ_TRASH_BYTES;
   l.slabs = (size_t)slabs * SPLITK_SLAB_BYTES;
-  l.total = l.meta + 5 * l.ptr + l.tiles + l.pdesc + l.pq + l.counters + l.trash + l.slabs;
+  l.total = l.meta + 5 * l.ptr + l.tiles + l.counters + l.slabs;
   return l;
 }
 
@@ -428,9 +373,6 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (lda_b < kbytes || ldb_b < kbytes || (lda_b % 16) || (ldb_b % 16))
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: lda/ldb must be >= K row and a multiple of 8 words", idx);
   if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
-  if (v.persistent && ((int64_t)p.M * lda_b >= (1LL << 31) || (int64_t)p.N * ldb_b >= (1LL << 31)))
-    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s addresses A / B with 32-bit offsets (< 2 GiB each)",
-                idx, v.name);
   if (check_ptrs && p.M > 0 && p.N > 0) {  // empty problems are dropped by the planner
     if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
     if (!is_float16(qt) && (!p.SA || !p.SB)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer", idx);
@@ -459,8 +401,6 @@ struct Plan {
   std::vector<TileDesc> tiles;  // indexed by blockIdx
   int total_tiles = 0;
   int slabs = 0;                // split-K partial slabs
-  int queue_len[8] = {0};       // valid tiles of XCD queue x (slots 8 i + x, i < len)
-  bool persistent = false;      // planned for a persistent variant (PTileDesc records in the image)
 };
 
 // Tile generation + scheduling.
@@ -475,7 +415,6 @@ struct Plan {
 int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptrs, Plan* plan) {
   const Variant& v = variants()[variant];
   const int P = (int)probs.size();
-  plan->persistent = v.persistent;
   std::vector<GGMeta> all(P);
   for (int i = 0; i < P; ++i) {
     int st = build_meta(probs[i], i, v, check_ptrs, &all[i]);
@@ -520,7 +459,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // whole call (low-fill calls: small batches, long-K shared experts, per-rank work lists) has its
   // tiles cut into split[i] K slices of >= 4 stages each, at most 8
   std::vector<int> split(P, 1);
-  if (v.kind == Kind::V2 && !v.persistent) {
+  if (v.kind == Kind::V2) {
     double total = 0;
     std::vector<double> biggest(P, 0.0);
     for (int i : order) {
@@ -656,7 +595,6 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   for (const auto& q : queue) qmax = std::max(qmax, q.size());
   int grid = 0;
   plan->tiles.assign(8 * qmax, TileDesc{-1, 0, 0, 0, 0, 0, -1, -1});
-  for (int x = 0; x < 8; ++x) plan->queue_len[x] = (int)queue[x].size();
   for (int x = 0; x < 8; ++x)
     for (size_t i = 0; i < queue[x].size(); ++i) {
       const int b = (int)(8 * i) + x;
@@ -735,36 +673,11 @@ std::vector<HostProblem> to_host(const mxmoe_gg_problem* problems, int problem_c
 // Host image of the workspace for a plan; pointer columns from `hp` in table-row order.
 std::vector<uint8_t> workspace_image(const Plan& plan, const std::vector<const void*> cols[5], WsLayout* out) {
   const int P = (int)plan.meta.size();
-  const WsLayout l = ws_layout(P, (int)plan.tiles.size(), plan.slabs, plan.persistent);
-  std::vector<uint8_t> img(l.image(), 0);  // queue heads and counters start at zero
+  const WsLayout l = ws_layout(P, (int)plan.tiles.size(), plan.slabs);
+  std::vector<uint8_t> img(l.total - l.slabs, 0);  // counters start at zero; slabs need no init
   memcpy(img.data(), plan.meta.data(), (size_t)P * sizeof(GGMeta));
   for (int c = 0; c < 5; ++c) memcpy(img.data() + l.meta + c * l.ptr, cols[c].data(), (size_t)P * sizeof(void*));
   memcpy(img.data() + l.meta + 5 * l.ptr, plan.tiles.data(), plan.tiles.size() * sizeof(TileDesc));
-  if (plan.persistent) {
-    PTileDesc* pd = reinterpret_cast<PTileDesc*>(img.data() + l.meta + 5 * l.ptr + l.tiles);
-    for (size_t b = 0; b < plan.tiles.size(); ++b) {
-      const TileDesc& td = plan.tiles[b];
-      if (td.prob < 0) continue;
-      const GGMeta& m = plan.meta[td.prob];
-      PTileDesc& d = pd[b];
-      d.A = static_cast<const uint8_t*>(cols[0][td.prob]);
-      d.B = static_cast<const uint8_t*>(cols[1][td.prob]);
-      d.SA = static_cast<const _Float16*>(cols[2][td.prob]);
-      d.SB = static_cast<const _Float16*>(cols[3][td.prob]);
-      d.C = static_cast<_Float16*>(const_cast<void*>(cols[4][td.prob]));
-      d.M = m.M;
-      d.N = m.N;
-      d.kbytes = m.kbytes;
-      d.qcls = m.qtype | ((td.cls & 0xFF) << 8);
-      d.lda_b = (int32_t)m.lda_b;
-      d.ldb_b = (int32_t)m.ldb_b;
-      d.ldc = (int32_t)m.ldc;
-      d.m0 = td.m0;
-      d.n0 = td.n0;
-    }
-  }
-  memcpy(img.data() + l.meta + 5 * l.ptr + l.tiles + l.pdesc + 16 * sizeof(int32_t), plan.queue_len,
-         sizeof(plan.queue_len));
   *out = l;
   return img;
 }
@@ -868,7 +781,7 @@ int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count,
   Plan plan;
   st = plan_host(hp, variant, false, &plan);
   if (st) return st;
-  *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size(), plan.slabs, plan.persistent).total;
+  *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size(), plan.slabs).total;
   return MXMOE_GG_OK;
 }
 
@@ -906,7 +819,7 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   if (st) return st;
   if (info->total_tiles == 0) return MXMOE_GG_OK;
   const int P = info->problem_count;
-  const WsLayout l = ws_layout(P, info->grid, info->splitk_slabs, variants()[info->variant].persistent);
+  const WsLayout l = ws_layout(P, info->grid, info->splitk_slabs);
   const uint8_t* ws = static_cast<const uint8_t*>(info->workspace);
   GGArgs a;
   a.meta = reinterpret_cast<const GGMeta*>(ws);
@@ -918,13 +831,8 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   a.ptr_C = reinterpret_cast<void* const*>(ws + l.meta + 4 * l.ptr);
   a.P = P;
   a.n_slots = info->grid;
-  uint8_t* base = const_cast<uint8_t*>(ws) + l.meta + 5 * l.ptr + l.tiles;
-  a.pdesc = reinterpret_cast<const PTileDesc*>(base);
-  base += l.pdesc;
-  a.pq = reinterpret_cast<int32_t*>(base);
-  a.counters = reinterpret_cast<int32_t*>(base + l.pq);
-  a.trash = base + l.pq + l.counters;
-  a.slabs = base + l.pq + l.counters + l.trash;
+  a.counters = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(ws) + l.meta + 5 * l.ptr + l.tiles);
+  a.slabs = const_cast<uint8_t*>(ws) + l.meta + 5 * l.ptr + l.tiles + l.counters;
   variants()[info->variant].launch(a, info->grid, info->qtype_mask, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return MXMOE_GG_OK;

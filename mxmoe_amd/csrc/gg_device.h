@@ -88,25 +88,7 @@ struct GGArgs {
   int32_t n_slots;  // gridDim.x
   uint8_t* slabs;     // split-K partial slabs (SPLITK_SLAB_BYTES each)
   int32_t* counters;  // split-K arrival counters (zero between launches)
-  int32_t* pq;        // persistent kernels: per-XCD queue heads [0, 8), done [8], lengths [16, 24)
-  uint8_t* trash;     // persistent kernels: sink of the masked-off epilogue stores (PQ_TRASH_BYTES)
-  const struct PTileDesc* pdesc;  // persistent kernels: one self-contained record per tile slot
 };
-// Persistent kernels read one 128-B record per tile (two scalar loads, no pointer chasing through
-// the plan table, few SGPRs): operand pointers, shape, strides (bytes / elements, < 2^31), origin.
-struct PTileDesc {
-  const uint8_t* A;
-  const uint8_t* B;
-  const _Float16* SA;
-  const _Float16* SB;
-  _Float16* C;
-  int32_t M, N, kbytes, qcls;  // qcls = qtype | height class << 8
-  int32_t lda_b, ldb_b, ldc, m0;
-  int32_t n0, pad_[13];
-};
-static_assert(sizeof(PTileDesc) == 128, "PTileDesc must stay 128 bytes");
-constexpr int PQ_BYTES = 256;                 // queue heads / done / lengths
-constexpr int PQ_TRASH_BYTES = 256 * 1024;    // 1 KiB per persistent workgroup
 
 typedef int32_t v2i __attribute__((ext_vector_type(2)));
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
@@ -594,37 +576,6 @@ __device__ __forceinline__ void v2_dma(const uint8_t* const (&src)[G], uint8_t* 
     for (int j = 0; j < G; ++j) {
       const int kc = (p ^ ((((wave * G + j) * 8 + rsub) >> 1) & 7)) << 4;
       glds16(kb + kc < kbytes ? src[j] + kb : zero, dst + (wave * G + j) * 1024);
-    }
-  }
-}
-
-// v2_dma through a buffer resource: the operand base lives in 4 SGPRs, each lane keeps one 32-bit
-// byte offset (a VGPR instead of a 64-bit pointer), the stage's K offset goes in soffset; K-tail
-// chunks get an offset past num_records (2^31), which the buffer unit returns as zeros — no zero
-// block, no pointer select. The planner keeps every operand of such a variant under 2 GiB.
-constexpr uint32_t SRD_OOB = 0xFFFFFF00u;
-// buffer_load ... lds of 16 B per lane from `base` + voff + soff (raw buffer, num_records 2^31)
-__device__ __forceinline__ void bglds16(const void* base, uint32_t voff, int soff, uint8_t* lds_dst) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x80000000, 0x00020000),
-      (lds_void_t*)lds_dst, 16, voff, soff, 0, 0);
-}
-template <int G>
-__device__ __forceinline__ void v2_dma_srd(const void* base, const uint32_t (&off)[G], uint8_t* dst, int kb, int kbytes,
-                                           int wave, int lane) {
-  if (kb + 128 <= kbytes) {
-#pragma unroll
-    for (int j = 0; j < G; ++j) bglds16(base, off[j], kb, dst + (wave * G + j) * 1024);
-  } else {
-    // (last stage only) the K chunk of each lane, recomputed here from an opaque lane id so the
-    // compiler does not hoist these per-lane values out of the K loop and keep them live in it
-    int ol = lane;
-    asm volatile("" : "+v"(ol));
-    const int rsub = ol >> 3, p = ol & 7;
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const int kc = (p ^ ((((wave * G + j) * 8 + rsub) >> 1) & 7)) << 4;
-      bglds16(base, kb + kc < kbytes ? off[j] : SRD_OOB, kb, dst + (wave * G + j) * 1024);
     }
   }
 }
@@ -1738,369 +1689,6 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   }
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
   epilogue_v3<Cfg, QT_F16>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
-}
-
-// ============================================================================================
-// v2p: the staggered v2 kernel made PERSISTENT — one 512-thread workgroup per CU loops over tiles,
-// so a tile's fixed costs overlap the next tile instead of idling the CU:
-//   * tiles come from the planner's per-XCD queues (XCD x's i-th tile = table slot 8 i + x) through
-//     one atomic head per queue; a workgroup pops from the queue of the XCD it runs on
-//     (HW_REG_XCC_ID) and, once that is empty, from the others — every slot is popped exactly once
-//     whatever the placement (placement is speed only). The next pop is issued at the start of the
-//     current tile (its latency hides under the mainloop); the last workgroup out re-zeroes the
-//     heads for the next launch;
-//   * at the end of a tile's mainloop the NEXT tile's prologue is issued — K stages 0 and 1 into
-//     both ring buffers — and only then the current tile's epilogue runs, with direct 8-B stores
-//     from registers (the ring is no longer free for staging); stage 0 of the next tile lands under
-//     the epilogue and the stores drain under the next tile's first two stages (vmcnt counts them:
-//     order stage 0, stage 1, stores — every store is issued, masked-off ones into a
-//     per-workgroup sink, so the counts are exact); the int paths' scales are loaded at a tile's
-//     start and stashed in LDS after its mainloop (alternating 1-KiB slots);
-//   * no inter-block gap, no prologue stall; the mainloop is v2s's (stagger, two 64-KiB stages).
-// fp16 / bf16 / w8a8 / w4a4 tiles (128-B K stages); no split-K (the planner does not split for it).
-// ============================================================================================
-constexpr int V2P_STASH = V2Cfg<256>::LDS_BYTES;           // 2 x 1 KiB scale stash slots
-constexpr int V2P_BCAST = V2Cfg<256>::LDS_BYTES + 2048;    // next-tile broadcast word
-
-// Queue pop in two halves so that nothing waits on the atomic inside a mainloop: pq_take issues the
-// returning fetch-add on the workgroup's own XCD queue (its result is first used after the tile's
-// last stage, when every older vector-memory op has been waited for anyway); pq_slot turns it into
-// a table slot, stealing from the other queues once the own one is empty (call tails only).
-__device__ __forceinline__ int pq_take(int32_t* pq, int xcc) {
-  return __hip_atomic_fetch_add(pq + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int pq_slot(int32_t* pq, int xcc, int taken, int own_len) {
-  if (taken < own_len) return 8 * taken + xcc;
-#pragma unroll 1
-  for (int q = 1; q < 8; ++q) {
-    const int x = (xcc + q) & 7;
-    const int i = __hip_atomic_fetch_add(pq + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (i < __hip_atomic_load(pq + 16 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 8 * i + x;
-  }
-  return -1;
-}
-
-// one tile's wave-uniform description (SGPRs)
-struct PTMeta {
-  int M, N, kbytes, qtype, lda_b, ldb_b, ldc;
-};
-struct PTile {
-  PTMeta mt;
-  const uint8_t* A;
-  const uint8_t* B;
-  const _Float16* SA;
-  const _Float16* SB;
-  _Float16* C;
-  int m0, n0, cls;
-};
-
-// The plan table is read-only for the whole launch, but after the kernel's own stores the compiler
-// can no longer prove that and emits VECTOR loads (VGPR results, and hipcc then waits vmcnt(0) at
-// their first use — draining the in-flight LDS-DMA). Explicit scalar loads keep the descriptor in
-// SGPRs and on lgkmcnt (the plan is written by the host before the launch; loads only).
-typedef int32_t s8i __attribute__((ext_vector_type(8)));
-typedef int32_t s16i __attribute__((ext_vector_type(16)));
-typedef int32_t s2i __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void p_load(const GGArgs& args, int slot, PTile& t) {
-  // loads AND their wait in one asm statement: the compiler must not read (or copy) the destination
-  // SGPRs before the scalar loads have landed; early-clobber keeps them off the address registers
-  s16i d;
-  s8i e;
-  const PTileDesc* rec = args.pdesc + slot;
-  asm volatile(
-      "s_load_dwordx16 %0, %2, 0x0\n\t"
-      "s_load_dwordx8 %1, %2, 0x40\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&s"(d), "=&s"(e)
-      : "s"(rec)
-      : "memory");
-  t.A = __builtin_bit_cast(const uint8_t*, s2i{d[0], d[1]});
-  t.B = __builtin_bit_cast(const uint8_t*, s2i{d[2], d[3]});
-  t.SA = __builtin_bit_cast(const _Float16*, s2i{d[4], d[5]});
-  t.SB = __builtin_bit_cast(const _Float16*, s2i{d[6], d[7]});
-  t.C = __builtin_bit_cast(_Float16*, s2i{d[8], d[9]});
-  t.mt.M = d[10];
-  t.mt.N = d[11];
-  t.mt.kbytes = d[12];
-  t.mt.qtype = d[13] & 0xFF;
-  t.cls = (d[13] >> 8) & 0xFF;
-  t.mt.lda_b = d[14];
-  t.mt.ldb_b = d[15];
-  t.mt.ldc = e[0];
-  t.m0 = e[1];
-  t.n0 = e[2];
-}
-
-// K stage s of tile t into ring buffer buf (64-KiB buffers; A at +0, B at +32 KiB for every
-// height class): GA = rows / 64 + GB = 4 LDS-DMA instructions per wave
-__device__ __forceinline__ void p_issue_stage(const PTile& t, int s, int buf, uint8_t* lds, int wave, int lane) {
-  const int ga = t.cls == 0 ? 4 : 2;
-  const int rsub = lane >> 3, p = lane & 7;
-  const int kb = s * 128;
-  uint8_t* As = lds + buf * 65536;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (j < ga) {
-      const int row = (wave * ga + j) * 8 + rsub;
-      const int kc = (p ^ ((row >> 1) & 7)) << 4;
-      const uint32_t off = (uint32_t)min(t.m0 + row, t.mt.M - 1) * (uint32_t)t.mt.lda_b + kc;
-      bglds16(t.A, kb + kc < t.mt.kbytes ? off : SRD_OOB, kb, As + (wave * ga + j) * 1024);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (wave * 4 + j) * 8 + rsub;
-    const int kc = (p ^ ((row >> 1) & 7)) << 4;
-    const uint32_t off = (uint32_t)min(t.n0 + row, t.mt.N - 1) * (uint32_t)t.mt.ldb_b + kc;
-    bglds16(t.B, kb + kc < t.mt.kbytes ? off : SRD_OOB, kb, As + 32768 + (wave * 4 + j) * 1024);
-  }
-}
-
-// The counted vmcnt waits of the persistent kernel assume the issue order stage 0, stage 1, stores:
-// keep the compiler from interleaving those vector-memory ops (the hardware keeps issue order)
-__device__ __forceinline__ void vm_order_fence() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// prologue of tile t: stage 0, stage 1 (if any) — in that order (vmcnt bookkeeping)
-__device__ __forceinline__ void p_prologue(const PTile& t, int slot, uint8_t* lds, int wave, int lane) {
-  (void)slot;
-  const int nst = (t.mt.kbytes + 127) / 128;
-  p_issue_stage(t, 0, 0, lds, wave, lane);
-  vm_order_fence();
-  if (nst > 1) p_issue_stage(t, 1, 1, lds, wave, lane);
-  vm_order_fence();
-}
-
-// DMA instructions per wave of stage 1 of tile t (0 if it has one stage)
-__device__ __forceinline__ int p_stage1_count(const PTile& t) {
-  return (t.mt.kbytes + 127) / 128 > 1 ? (t.cls == 0 ? 8 : 6) : 0;
-}
-
-// wait until at most `n` of this wave's vector-memory ops are outstanding (n from a small set)
-__device__ __forceinline__ void p_wait(int n) {
-  switch (n) {
-    case 0: wait_vmcnt<0>(); break;
-    case 6: wait_vmcnt<6>(); break;
-    case 8: wait_vmcnt<8>(); break;
-    case 14: wait_vmcnt<14>(); break;
-    case 16: wait_vmcnt<16>(); break;
-    case 22: wait_vmcnt<22>(); break;
-    case 24: wait_vmcnt<24>(); break;
-    default: wait_vmcnt<0>(); break;
-  }
-}
-
-// One persistent tile: stages 0 and 1 are in flight (stage 0 landed and published by the caller's
-// barrier), `st_prev` of this wave's stores of the previous tile are younger than stage 1.
-// Returns the next tile's slot (its prologue issued, its stage 0 landed and published), or -1.
-template <class Cfg, int QT, int ABL>
-__device__ __forceinline__ int p_tile(const GGArgs& args, PTile& t, uint8_t* lds, int& slot, int& st_prev,
-                                      int taken, int xcc, int own_len) {
-  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
-  typedef typename AccT<QT>::type acc_t;
-  typedef V2Half<Cfg, QT> Half;
-  // lane constants derived from an opaque copy of the thread id: the compiler cannot hoist them out
-  // of the persistent tile loop (where they would stay live — and spilled — across every tile)
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
-  const int r16 = lane & 15, g = lane >> 4;
-  const PTMeta& mt = t.mt;
-  const int nst = (mt.kbytes + 127) / 128;
-
-  uint32_t offA[GA], offB[GB];  // per-lane byte offsets from the operand bases (planner: < 2 GiB)
-  {
-    const int rsub = lane >> 3, p = lane & 7;
-#pragma unroll
-    for (int j = 0; j < GA; ++j) {
-      const int row = (wave * GA + j) * 8 + rsub;
-      offA[j] = (uint32_t)min(t.m0 + row, mt.M - 1) * (uint32_t)mt.lda_b + ((p ^ ((row >> 1) & 7)) << 4);
-    }
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-      const int row = (wave * GB + j) * 8 + rsub;
-      offB[j] = (uint32_t)min(t.n0 + row, mt.N - 1) * (uint32_t)mt.ldb_b + ((p ^ ((row >> 1) & 7)) << 4);
-    }
-  }
-  auto issue = [&](int s, int buf) {
-    uint8_t* As = lds + buf * 65536;
-    v2_dma_srd<GA>(t.A, offA, As, s * 128, mt.kbytes, wave, lane);
-    v2_dma_srd<GB>(t.B, offB, As + 32768, s * 128, mt.kbytes, wave, lane);
-  };
-  acc_t acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
-  const int swz = (r16 >> 1) & 7;
-  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
-  const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
-  auto hread = [&](Half& f, int buf, int h) { f.read(lds + buf * 65536, lds + buf * 65536 + 32768, a_row, b_row, swz, g, h); };
-  // int paths: this tile's row / column scales, loaded now and stashed in LDS after the mainloop (the
-  // first use of the load is then behind the last stage's full wait: no early vmcnt(0))
-  _Float16 sc = 0;
-  if constexpr (qt_scaled(QT)) {
-    if (tid < Cfg::BM) sc = t.SA[min(t.m0 + tid, mt.M - 1)];
-    else if (tid >= 256) sc = t.SB[min(t.n0 + tid - 256, mt.N - 1)];
-  }
-  // end of stage s: stage s+1 landed for every wave, buffer s & 1 released. Stage 0's wait leaves
-  // the previous tile's stores (younger than stage 1) in flight.
-  auto stage_sync = [&](int s) {
-    if (s == 0) p_wait(st_prev);
-    else wait_vmcnt<0>();
-    lds_barrier();
-  };
-  {
-    Half fr;
-    if (wave >= Cfg::WM * Cfg::WN / 2) {
-      for (int s = 0; s < nst; ++s) {
-        if (s >= 1 && s + 1 < nst) issue(s + 1, (s + 1) & 1);
-        if (s > 0) fr.mma(acc);
-        hread(fr, s & 1, 0);
-        fr.mma(acc);
-        hread(fr, s & 1, 1);
-        stage_sync(s);
-      }
-      fr.mma(acc);
-    } else {
-      for (int s = 0; s < nst; ++s) {
-        if (s >= 1 && s + 1 < nst) issue(s + 1, (s + 1) & 1);
-        hread(fr, s & 1, 0);
-        fr.mma(acc);
-        hread(fr, s & 1, 1);
-        fr.mma(acc);
-        stage_sync(s);
-      }
-    }
-  }
-  if constexpr (qt_scaled(QT)) {
-    if (tid < Cfg::BM || tid >= 256) reinterpret_cast<_Float16*>(lds + V2P_STASH + slot * 1024)[tid] = sc;
-  }
-  // the ring is free (every wave passed the last stage barrier); publish the next tile (the same
-  // barrier publishes the scale stash)
-  int* bslot = reinterpret_cast<int*>(lds + V2P_BCAST);
-  if (tid == 0) *bslot = pq_slot(args.pq, xcc, taken, own_len);
-  lds_barrier();
-  const int nxt = __builtin_amdgcn_readfirstlane(*bslot);
-  PTile tn;
-  int s1n = 0;
-  if (nxt >= 0) {
-    p_load(args, nxt, tn);
-    p_prologue(tn, slot ^ 1, lds, wave, lane);
-    s1n = p_stage1_count(tn);
-  }
-  vm_order_fence();  // no epilogue store may be scheduled above the next tile's DMA
-
-  // ---- epilogue: direct 8-B stores from registers (lane: row 16 i + r16, columns 16 j + 4 g..+3) ----
-  int etid = threadIdx.x;
-  asm volatile("" : "+v"(etid));
-  const int e_lane = etid & 63, e_r16 = e_lane & 15, e_g = e_lane >> 4;
-  const _Float16* sl = reinterpret_cast<const _Float16*>(lds + V2P_STASH + slot * 1024);
-  const int mrow0 = t.m0 + wm * Cfg::WTM, ncol0 = t.n0 + wn * Cfg::WTN;
-  uint2 sbw[FN];
-  if constexpr (qt_scaled(QT)) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * e_g);
-  }
-  // 16-B stores without LDS staging (the ring holds the next tile): for fragment columns j, j+1 a
-  // lane holds 4 columns of each; v_permlane16_swap (odd 16-lane rows of the first operand <-> even
-  // rows of the second) leaves lane group g with 8 consecutive columns of one row — block j columns
-  // 0-7 / 8-15 for g = 0 / 2, block j+1's for g = 1 / 3 — one dwordx4 per lane (16 rows x 64 B
-  // per instruction). Global stores: a flat store would also count in lgkmcnt, out of order.
-  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(1))) u4v guint4;
-  guint4* sink = (guint4*)(args.trash + (blockIdx.x & 255) * 1024 + e_lane * 16);
-  const int colofs = 8 * (e_g >> 1) + 16 * (e_g & 1);
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int ml = i * 16 + e_r16;
-    _Float16 sai = 0;
-    if constexpr (qt_scaled(QT)) sai = sl[wm * Cfg::WTM + ml];
-    const int m = mrow0 + ml;
-#pragma unroll
-    for (int jp = 0; jp < FN / 2; ++jp) {
-      uint2 p0, p1;
-      if constexpr (QT == QT_F16 || QT == QT_BF16) {
-        p0 = pack4_f16(acc[i][2 * jp]);
-        p1 = pack4_f16(acc[i][2 * jp + 1]);
-      } else {
-        p0 = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][2 * jp], sai, sbw[2 * jp]);
-        p1 = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][2 * jp + 1], sai, sbw[2 * jp + 1]);
-      }
-      const auto sx = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
-      const auto sy = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
-      const int n = ncol0 + jp * 32 + colofs;
-      // every lane stores (masked-off ones into the sink): exactly FM * FN / 2 stores per wave
-      guint4* dst = (m < mt.M && n < mt.N) ? (guint4*)(t.C + (int64_t)m * mt.ldc + n) : sink;
-      *dst = u4v{sx[0], sy[0], sx[1], sy[1]};
-    }
-  }
-  vm_order_fence();
-  if (nxt < 0) return -1;
-  // next tile's stage 0 landed: younger are its stage 1 and this tile's stores
-  p_wait(s1n + FM * FN / 2);
-  lds_barrier();  // (not __syncthreads: its fence would wait for stage 1 and the stores)
-  st_prev = s1n > 0 ? FM * FN / 2 : 0;
-  slot ^= 1;
-  t = tn;
-  return nxt;
-}
-
-template <int ABL, int QM>
-__global__ __launch_bounds__(512, 2) void gg_v2p_kernel(GGArgs args) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int xcc = __builtin_amdgcn_s_getreg((19 << 11) | 20) & 7;  // HW_REG_XCC_ID
-  int* bslot = reinterpret_cast<int*>(lds + V2P_BCAST);
-  int own_len = 0;
-  if (tid == 0) {
-    own_len = __hip_atomic_load(args.pq + 16 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *bslot = pq_slot(args.pq, xcc, pq_take(args.pq, xcc), own_len);
-  }
-  __syncthreads();
-  int cur = __builtin_amdgcn_readfirstlane(*bslot);
-  if (cur >= 0) {
-    PTile t;
-    p_load(args, cur, t);
-    int slot = 0, st_prev = 0;
-    p_prologue(t, slot, lds, wave, lane);
-    wait_vmcnt<0>();
-    lds_barrier();
-    while (cur >= 0) {
-      int taken = 0;
-      if (tid == 0) taken = pq_take(args.pq, xcc);  // first used after this tile's mainloop
-      const int qt = t.mt.qtype;
-      if ((QM & (1 << QT_I8)) && qt == QT_I8) {
-        cur = t.cls == 0 ? p_tile<V2Cfg<256>, QT_I8, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len)
-                         : p_tile<V2Cfg<128>, QT_I8, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len);
-      } else if ((QM & (1 << QT_I4)) && qt == QT_I4) {
-        cur = t.cls == 0 ? p_tile<V2Cfg<256>, QT_I4, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len)
-                         : p_tile<V2Cfg<128>, QT_I4, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len);
-      } else if ((QM & (1 << QT_BF16)) && qt == QT_BF16) {
-        cur = t.cls == 0 ? p_tile<V2Cfg<256>, QT_BF16, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len)
-                         : p_tile<V2Cfg<128>, QT_BF16, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len);
-      } else if ((QM & (1 << QT_F16)) && qt == QT_F16) {
-        cur = t.cls == 0 ? p_tile<V2Cfg<256>, QT_F16, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len)
-                         : p_tile<V2Cfg<128>, QT_F16, ABL>(args, t, lds, slot, st_prev, taken, xcc, own_len);
-      } else {
-        cur = -1;  // (unreachable: the planner admits only the types above for this variant)
-      }
-    }
-  }
-  // last workgroup out re-zeroes the queue heads for the next launch (every pop is done by then)
-  if (tid == 0) {
-    const int d = __hip_atomic_fetch_add(args.pq + 8, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == (int)gridDim.x - 1) {
-#pragma unroll
-      for (int x = 0; x < 8; ++x) __hip_atomic_store(args.pq + x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(args.pq + 8, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel

@@ -98,7 +98,7 @@ def test_weightonly_only_on_v2_variants():
     for ln in nat.list_variants():
         vid, name = int(ln.split()[0]), ln.split()[1]
         st, err = _plan([_prob()], vid)
-        if name.startswith(("v2", "abl_v2")) and not name.startswith("v2p"):  # v2p: 128-B-stage types only
+        if name.startswith(("v2", "abl_v2")):
             assert st == nat.MXMOE_GG_ERR_WORKSPACE, (name, err)  # validation passed, no workspace given
             assert "w4a16=TileConfig(BM=256, BN=256, BK=64" in ln and "w8a16=TileConfig(" in ln
         else:
