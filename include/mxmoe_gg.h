@@ -195,6 +195,15 @@ int mxmoe_gg_repack_weightonly(const uint16_t* ref_words, int N, int K, int w_bi
  * min(bytes, 1 MiB) into host memory `dst` (synchronous); reset != 0 then zeroes the record. */
 int mxmoe_gg_debug_trace(void* dst, size_t bytes, int reset);
 
+/* Diagnostics (no reference counterpart): the host tile table mxmoe_gg_plan would upload, without
+ * touching a device — 8 int32 per workgroup slot {table row (-1 = empty slot), m0, n0, class
+ * (bits 8-15 split-K slice, 16-23 slices), first K stage, end K stage, split-K slab, split-K group},
+ * blockIdx order (XCD x runs slots x, x + 8, ...); `rows` (optional, problem_count int32) receives
+ * the caller's problem index of every table row. Writes min(*slots, needed) slots and sets *slots
+ * to the number needed. */
+int mxmoe_gg_plan_tiles(const mxmoe_gg_problem* problems, int problem_count, int variant, int32_t* tiles,
+                        int32_t* rows, int* slots);
+
 #ifdef __cplusplus
 }
 #endif

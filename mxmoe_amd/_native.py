@@ -79,6 +79,7 @@ EXPORTED_SYMBOLS = (
     "mxmoe_gg_list_variants",
     "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
     "groupgemm_mxmoe", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
+    "mxmoe_gg_plan_tiles",
     # include/mxmoe_moe.h (MoE-layer plumbing)
     "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_combine",
 )
@@ -127,6 +128,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_repack_weightonly.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_void_p]
     lib.mxmoe_gg_debug_trace.restype = c.c_int
     lib.mxmoe_gg_debug_trace.argtypes = [c.c_void_p, c.c_size_t, c.c_int]
+    lib.mxmoe_gg_plan_tiles.restype = c.c_int
+    lib.mxmoe_gg_plan_tiles.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.c_void_p, c.c_void_p,
+                                        c.POINTER(c.c_int)]
     P = c.c_void_p
     lib.mxmoe_moe_route.restype = c.c_int
     lib.mxmoe_moe_route.argtypes = [P, c.c_int64, c.c_int, c.c_int, P, P, P, P, P]
@@ -181,6 +185,22 @@ def variant_count() -> int:
 def production_variants() -> list[int]:
     """Compiled variants that compute correct results (``abl_*`` are timing ablations)."""
     return [int(ln.split()[0]) for ln in list_variants() if not ln.split()[1].startswith("abl_")]
+
+
+def plan_tiles(problems, variant: int):
+    """Host tile table of a plan (mxmoe_gg_plan_tiles; no device needed): (tiles [slots, 8] int32
+    with columns prob/m0/n0/cls/ks0/ks1/slab/grp in blockIdx order, rows: table row -> the caller's
+    problem index)."""
+    import numpy as np
+
+    P = len(problems)
+    arr = (GGProblemC * P)(*problems)
+    n = ctypes.c_int(0)
+    check(lib().mxmoe_gg_plan_tiles(arr, P, variant, None, None, ctypes.byref(n)))
+    tiles = np.zeros((n.value, 8), dtype=np.int32)
+    rows = np.full(P, -1, dtype=np.int32)
+    check(lib().mxmoe_gg_plan_tiles(arr, P, variant, tiles.ctypes.data, rows.ctypes.data, ctypes.byref(n)))
+    return tiles, rows
 
 
 def default_variant() -> int:

@@ -408,10 +408,12 @@ struct Plan {
 //     then one tail_bm (128) or tail2_bm (64) tile), n-tiles of width bn; 4-m-tile bands, n-major
 //     inside a band, so 32 consecutive tiles form a ~4 x 8 block sharing A rows and B columns;
 //  2. problems by descending per-tile cost (K bytes x tile area x MFMA passes), longest first;
-//  3. the sequence is cut into chunks of `chunk` tiles; each chunk in turn joins the queue of the
-//     XCD with the least modelled time so far (tile_time); XCD x's i-th tile is blockIdx 8 i + x
-//     (blocks b and b + 8 share an XCD under the round-robin dispatch; placement affects speed
-//     only, never results).
+//  3. XCD regions: a problem of >= 8 chunks of tiles (the shared expert at large batch) is cut
+//     into 8 rectangles of its tile grid, one per XCD, at the head of that XCD's queue (region_of);
+//  4. the rest is cut into chunks of about `chunk` tiles that do not straddle problems; each chunk
+//     in turn joins the queue of the XCD with the least modelled time so far (tile_time); XCD x's
+//     i-th tile is blockIdx 8 i + x (blocks b and b + 8 share an XCD under the round-robin
+//     dispatch; placement affects speed and HBM traffic only, never results).
 int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptrs, Plan* plan) {
   const Variant& v = variants()[variant];
   const int P = (int)probs.size();
@@ -509,14 +511,76 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   plan->meta.clear();
   plan->order = order;
   plan->slabs = 0;
+  const int chunk = v.chunk;
+  // XCD regions. Within one XCD, consecutive tiles run together (the XCD hands each freed CU its
+  // next block), so a band's A rows and B columns are re-read from that XCD's L2 while they are
+  // hot; but under chunked LPT a 4-m-tile band of the 44 n-tile shared expert lands on ~5 XCDs and
+  // each fetches the band's A panels again (and every band its B panels): 528 MB of panel reads
+  // for 78 MB of operands at bs=8192. One rectangle per XCD (r m-tiles x c n-tiles, enumerated in
+  // bands of `band` along the cheaper axis) reads r A panels + ceil(r / band) * c B panels (or the
+  // transpose) — the split of the grid into 8 rectangles is chosen to minimise that sum.
+  const char* region_env = getenv("MXMOE_GG_REGION");  // A/B switch (default on)
+  const bool regions_on = !(region_env && region_env[0] == '0');
+  struct Region {
+    int gm = 0, gn = 0, r = 0, c = 0;
+    bool nband = false;  // true: bands of n-tiles, m-major inside
+  };
+  auto region_of = [&](int i, Region* out) {
+    const GGMeta& m = all[i];
+    const int mt = (int)m_tiles(m).size(), nt = m.tiles_n;
+    if (!regions_on || v.kind != Kind::V2 || split[i] != 1 || (int64_t)mt * nt < 8 * (int64_t)chunk) return false;
+    const TileGeom& g = v.geom[m.qtype];
+    const double a_panel = (double)g.bm * m.kbytes, b_panel = (double)g.bn * m.K * probs[i].w_bits / 8.0;
+    double best = 0;
+    for (int gm = 1; gm <= 8; gm *= 2) {
+      const int gn = 8 / gm;
+      if (mt < gm || nt < gn) continue;
+      const int r = (mt + gm - 1) / gm, c = (nt + gn - 1) / gn;
+      // every region non-empty and within 25 % of the largest (the LPT fill evens out the rest)
+      const int r_last = mt - (gm - 1) * r, c_last = nt - (gn - 1) * c;
+      if (r_last <= 0 || c_last <= 0 || 4 * (int64_t)r_last * c_last < 3 * (int64_t)r * c) continue;
+      const int b = (int)band;
+      const double mband = r * a_panel + (double)((r + b - 1) / b) * c * b_panel;
+      const double nband = c * b_panel + (double)((c + b - 1) / b) * r * a_panel;
+      const double cost = std::min(mband, nband);
+      if (out->gm == 0 || cost < best) {
+        *out = Region{gm, gn, r, c, nband < mband};
+        best = cost;
+      }
+    }
+    return out->gm != 0;
+  };
   int groups = 0;
-  std::vector<TileDesc> seq;
+  std::vector<TileDesc> seq;                // chunked tiles
+  std::vector<int> seq_end;                 // per seq tile: end of its problem's run in seq
+  std::vector<std::vector<TileDesc>> region_tiles(8);  // per XCD
   for (int row = 0; row < (int)order.size(); ++row) {
     GGMeta m = all[order[row]];
     const TileGeom& g = v.geom[m.qtype];
     const std::vector<std::pair<int, int>> mt = m_tiles(m);  // (m0, cls)
     m.tile_begin = (int32_t)seq.size();
     const int nt = m.tiles_n, S = split[order[row]], nst = stages_of(m);
+    Region rg;
+    if (region_of(order[row], &rg)) {
+      for (int x = 0; x < 8; ++x) {
+        const int mb0 = (x / rg.gn) * rg.r, mb1 = std::min((int)mt.size(), mb0 + rg.r);
+        const int nb0 = (x % rg.gn) * rg.c, nb1 = std::min(nt, nb0 + rg.c);
+        auto put = [&](int mi, int n) {
+          region_tiles[x].push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second, 0, nst, -1, -1});
+        };
+        if (rg.nband) {
+          for (int nb = nb0; nb < nb1; nb += (int)band)
+            for (int mi = mb0; mi < mb1; ++mi)
+              for (int n = nb; n < std::min(nb1, nb + (int)band); ++n) put(mi, n);
+        } else {
+          for (int mb = mb0; mb < mb1; mb += (int)band)
+            for (int n = nb0; n < nb1; ++n)
+              for (int mi = mb; mi < std::min(mb1, mb + (int)band); ++mi) put(mi, n);
+        }
+      }
+      plan->meta.push_back(m);
+      continue;
+    }
     for (size_t mb = 0; mb < mt.size(); mb += band)
       for (int n = 0; n < nt; ++n)
         for (size_t mi = mb; mi < std::min(mt.size(), mb + band); ++mi) {
@@ -530,9 +594,12 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
             seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second | (k << 8) | (S << 16),
                                    k * nst / S, (k + 1) * nst / S, slab, grp});
         }
+    seq_end.resize(seq.size(), (int)seq.size());
     plan->meta.push_back(m);
   }
-  const int T = (int)seq.size();
+  size_t T_head = 0;
+  for (const auto& h : region_tiles) T_head += h.size();
+  const int T = (int)(seq.size() + T_head);
   if (T > (1 << 28)) return fail(MXMOE_GG_ERR_INVALID, "too many tiles (%d)", T);
   auto tile_time = [&](const TileDesc& td) {
     return stage_time(plan->meta[td.prob], td.cls & 0xFF) * (td.ks1 - td.ks0);
@@ -543,7 +610,6 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // every XCD simulated as `chunk` workgroup slots taking its queue in order, as the hardware
   // hands a freed slot the XCD's next block. Plain round-robin chunks let a low-fill call's few
   // long tiles pile onto 2-3 XCDs (bs=512: per-XCD busy time 40 % apart).
-  const int chunk = v.chunk;
   struct XcdSim {
     std::vector<double> slot;  // min-heap of slot free times
     double finish = 0, load = 0;
@@ -557,15 +623,30 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   };
   std::vector<XcdSim> sim(8);
   for (auto& x : sim) x.slot.assign(chunk, 0.0);
-  std::vector<std::vector<int>> queue(8);
+  std::vector<std::vector<int>> queue(8);  // indices into `all_tiles`: region tiles first, then chunks
+  std::vector<TileDesc> all_tiles(seq);
+  for (int x = 0; x < 8; ++x)
+    for (const TileDesc& td : region_tiles[x]) {
+      sim[x].add(tile_time(td));
+      queue[x].push_back((int)all_tiles.size());
+      all_tiles.push_back(td);
+    }
+  const int TS = (int)seq.size();
   const char* tc_env = getenv("MXMOE_GG_TAIL_CHUNK");  // A/B switch: tail chunk size (default 16)
   const int tail_chunk = tc_env && atoi(tc_env) > 0 ? atoi(tc_env) : 16;
   const char* rr_env = getenv("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
   const bool round_robin = rr_env && rr_env[0] == '1';
-  for (int s0 = 0, c = 0; s0 < T; ++c) {
-    const bool head = T - s0 > 16 * chunk;
-    const int len = (round_robin || head) ? chunk : std::min(chunk, tail_chunk);
-    const int s1 = std::min(T, s0 + len);
+  for (int s0 = 0, c = 0; s0 < TS; ++c) {
+    const bool head = TS - s0 > 16 * chunk;
+    int len = (round_robin || head) ? chunk : std::min(chunk, tail_chunk);
+    if (head && !round_robin && regions_on) {
+      // whole problems per chunk: split the rest of this problem's run into near-equal chunks of
+      // about `chunk` tiles (a 33-tile expert stays on one XCD instead of spilling 1 tile onto
+      // another that re-fetches its A rows), at most 64
+      const int rem = seq_end[s0] - s0, nc = std::max(1, (rem + chunk / 2) / chunk);
+      len = std::min(64, (rem + nc - 1) / nc);
+    }
+    const int s1 = std::min(TS, s0 + len);
     double times[64];
     for (int s = s0; s < s1; ++s) times[s - s0] = tile_time(seq[s]);
     int best = c % 8;
@@ -598,7 +679,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   for (int x = 0; x < 8; ++x)
     for (size_t i = 0; i < queue[x].size(); ++i) {
       const int b = (int)(8 * i) + x;
-      plan->tiles[b] = seq[queue[x][i]];
+      plan->tiles[b] = all_tiles[queue[x][i]];
       grid = std::max(grid, b + 1);
     }
   plan->tiles.resize(grid);
@@ -782,6 +863,24 @@ int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count,
   st = plan_host(hp, variant, false, &plan);
   if (st) return st;
   *bytes = ws_layout((int)plan.meta.size(), (int)plan.tiles.size(), plan.slabs).total;
+  return MXMOE_GG_OK;
+}
+
+int mxmoe_gg_plan_tiles(const mxmoe_gg_problem* problems, int problem_count, int variant, int32_t* tiles,
+                        int32_t* rows, int* slots) {
+  if (problem_count < 0 || (problem_count > 0 && !problems) || !slots || *slots < 0 || (*slots > 0 && !tiles))
+    return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_plan_tiles");
+  const std::vector<HostProblem> hp = to_host(problems, problem_count);
+  int st = resolve_variant(variant, hp, &variant);
+  if (st) return st;
+  Plan plan;
+  st = plan_host(hp, variant, false, &plan);
+  if (st) return st;
+  const int n = std::min(*slots, (int)plan.tiles.size());
+  if (n > 0) memcpy(tiles, plan.tiles.data(), (size_t)n * sizeof(TileDesc));
+  if (rows)
+    for (size_t r = 0; r < plan.order.size(); ++r) rows[r] = plan.order[r];
+  *slots = (int)plan.tiles.size();
   return MXMOE_GG_OK;
 }
 

@@ -1,0 +1,138 @@
+"""CPU tests of the host tile planner (gg_api.hip:plan_host) through mxmoe_gg_plan_tiles: every
+output tile of every problem is planned exactly once (split-K slices partition its K stages), and
+the placement rules hold — the shared expert of a bs=8192 layer is cut into one rectangle per XCD at
+the head of that XCD's queue, and routed experts are not split across XCDs by chunk boundaries.
+(The reference's TileScheduler, tile_scheduler.cuh:5-50, walks problems in order on the device; the
+placement is ours and affects speed and HBM traffic only, never results.)
+"""
+from __future__ import annotations
+
+import collections
+import ctypes
+
+import numpy as np
+import pytest
+
+from mxmoe_amd import _native as nat
+from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, model_workload, qwen2_layer11_workload
+
+FMT = {"": nat.FMT_DEFAULT, "E4M3": nat.FMT_E4M3, "bf16": nat.FMT_BF16}
+
+
+def _probs(shapes):
+    return [nat.GGProblemC(A=0, B=0, scale_a=0, scale_b=0, C=0, M=s.M, N=s.N, K=s.K, a_bits=s.a_bits,
+                           w_bits=s.w_bits, gsize=s.gsize, sym=int(s.sym), fmt=FMT[s.fmt], lda=0, ldb=0, ldc=0)
+            for s in shapes]
+
+
+def _bn(variant, s):
+    bm, bn, bk, th = (ctypes.c_int32() for _ in range(4))
+    nat.check(nat.lib().mxmoe_gg_variant_tile(variant, s.a_bits, s.w_bits, *(ctypes.byref(x) for x in (bm, bn, bk, th))))
+    return bm.value, bn.value
+
+
+def _layer(bs=8192, **kw):
+    return load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
+
+
+def check_coverage(shapes, variant=nat.VARIANT_AUTO):
+    probs = _probs(shapes)
+    v = nat.resolve_variant((nat.GGProblemC * len(probs))(*probs), len(probs), variant)
+    tiles, rows = nat.plan_tiles(probs, v)
+    live = tiles[tiles[:, 0] >= 0]
+    assert len({tuple(t) for t in live.tolist()}) == len(live), "a tile slot is planned twice"
+    by_prob = collections.defaultdict(list)
+    for t in live:
+        by_prob[int(rows[t[0]])].append(t)
+    for i, s in enumerate(shapes):
+        if s.M == 0 or s.N == 0:
+            assert i not in by_prob
+            continue
+        ts = np.array(by_prob[i])
+        bm, bn = _bn(v, s)
+        m0s = np.unique(ts[:, 1])
+        n0s = np.unique(ts[:, 2])
+        assert m0s[0] == 0 and m0s[-1] < s.M and (np.diff(m0s) <= bm).all() and (np.diff(m0s) > 0).all()
+        assert (n0s == np.arange(0, s.N, bn)).all(), f"problem {i}: n-tiles {n0s}"
+        ks_end = None
+        for m0 in m0s:
+            for n0 in n0s:
+                sl = ts[(ts[:, 1] == m0) & (ts[:, 2] == n0)]
+                assert len(sl) >= 1, f"problem {i}: tile ({m0}, {n0}) missing"
+                sl = sl[np.argsort(sl[:, 4])]
+                assert sl[0, 4] == 0 and (sl[1:, 4] == sl[:-1, 5]).all()
+                assert ks_end is None or sl[-1, 5] == ks_end
+                ks_end = sl[-1, 5]
+                if len(sl) > 1:  # split-K: one slab group, slice index / count in cls
+                    assert len(set(sl[:, 7].tolist())) == 1 and ((sl[:, 3] >> 16) & 0xFF == len(sl)).all()
+                    assert sorted(((sl[:, 3] >> 8) & 0xFF).tolist()) == list(range(len(sl)))
+                else:
+                    assert sl[0, 6] == -1 and sl[0, 7] == -1
+        assert len(ts) == sum(len(ts[(ts[:, 1] == m0) & (ts[:, 2] == n0)]) for m0 in m0s for n0 in n0s)
+    return tiles, rows, v
+
+
+@pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed", "e4m3", "w4a16"])
+@pytest.mark.parametrize("bs", [8192, 512])
+def test_every_tile_planned_once(cfg, bs):
+    kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
+          "mixed": dict(qconfig=mixed_qconfig_lp1()), "e4m3": dict(qstr="w8a8_g-1_sym_E4M3"),
+          "w4a16": dict(qstr="w4a16_g128_asym")}[cfg]
+    layer = _layer(bs, **kw)
+    for gg in ("gate_up", "down"):
+        check_coverage(layer[gg])
+
+
+def test_other_models_and_every_v2_variant():
+    for model in ("ds2", "mixtral", "qwen2_moe_57b"):
+        layer = next(iter(load_workload(model_workload(model, 4096)).values()))
+        for gg in ("gate_up", "down"):
+            check_coverage(layer[gg])
+    shapes = _layer(8192)["gate_up"]
+    for v in nat.production_variants():
+        check_coverage(shapes, v)
+
+
+def _xcd_queues(tiles):
+    q = [[] for _ in range(8)]
+    for b, t in enumerate(tiles):
+        if t[0] >= 0:
+            q[b % 8].append(t)
+    return q
+
+
+def test_shared_expert_one_rectangle_per_xcd(monkeypatch):
+    shapes = _layer(8192)["gate_up"]  # the shared expert is the last problem: 32 x 44 tiles
+    tiles, rows, v = check_coverage(shapes, nat.default_variant())
+    shared = len(shapes) - 1
+    q = _xcd_queues(tiles)
+    for x in range(8):
+        is_shared = [int(rows[t[0]]) == shared for t in q[x]]
+        n = sum(is_shared)
+        assert n == 32 * 44 // 8
+        assert all(is_shared[:n]) and not any(is_shared[n:]), "region tiles must head the XCD queue"
+        st = np.array([t for t, s in zip(q[x], is_shared) if s])
+        m_panels, n_panels = len(np.unique(st[:, 1])), len(np.unique(st[:, 2]))
+        # a rectangle: every (m, n) pair of its rows x columns
+        assert m_panels * n_panels == n
+        assert m_panels + n_panels <= 48  # 4 x 44 (vs 32 + 44 for a region of whole rows)
+    # A/B switch: without regions the shared expert is chunked across XCDs like any problem
+    monkeypatch.setenv("MXMOE_GG_REGION", "0")
+    tiles0, rows0 = nat.plan_tiles(_probs(shapes), v)
+    q0 = _xcd_queues(tiles0)
+    assert any(int(rows0[q0[x][0][0]]) != shared for x in range(8))
+
+
+def test_routed_experts_stay_on_one_xcd():
+    shapes = _layer(8192)["gate_up"]
+    tiles, rows, _ = check_coverage(shapes, nat.default_variant())
+    homes = collections.defaultdict(set)
+    for b, t in enumerate(tiles):
+        if t[0] >= 0:
+            homes[int(rows[t[0]])].add(b % 8)
+    routed = [i for i in range(len(shapes) - 1) if shapes[i].M > 0]
+    on_one = sum(len(homes[i]) == 1 for i in routed)
+    # the last 16 chunks' worth of tiles (~15 of the 60 experts here) are cut into 16-tile chunks on
+    # purpose, to even out the XCDs' finish; every expert before them stays whole
+    assert on_one >= 40, f"{on_one} of {len(routed)} routed experts on one XCD"
+    assert all(len(homes[i]) <= 3 for i in routed)

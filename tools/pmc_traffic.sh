@@ -5,7 +5,7 @@
 # usage: bash tools/pmc_traffic.sh <cfg...>     -> gpurun_out/pmc_traffic/pmc_traffic.json
 set -o pipefail
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$REPO/gpurun_out/pmc_traffic
+OUT=$REPO/${PMC_OUT:-gpurun_out/pmc_traffic}
 mkdir -p $OUT
 cd $REPO
 export TMPDIR=/tmp
