@@ -519,8 +519,13 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // for 78 MB of operands at bs=8192. One rectangle per XCD (r m-tiles x c n-tiles, enumerated in
   // bands of `band` along the cheaper axis) reads r A panels + ceil(r / band) * c B panels (or the
   // transpose) — the split of the grid into 8 rectangles is chosen to minimise that sum.
-  const char* region_env = getenv("MXMOE_GG_REGION");  // A/B switch (default on)
+  // placement: after the chunked tiles (default; measured 1-5 % faster than at the queue head on the
+  // w8a8 gate_up / down / mixed calls, profiles/r02/region/)
+  const char* region_env = getenv("MXMOE_GG_REGION");  // A/B switch: 0 off, 1 queue head, 2 tail (default)
   const bool regions_on = !(region_env && region_env[0] == '0');
+  const bool regions_last = !(region_env && region_env[0] == '1');
+  const char* align_env = getenv("MXMOE_GG_ALIGN");  // A/B switch: problem-aligned chunks (default on)
+  const bool align_on = !(align_env && align_env[0] == '0');
   struct Region {
     int gm = 0, gn = 0, r = 0, c = 0;
     bool nband = false;  // true: bands of n-tiles, m-major inside
@@ -625,12 +630,15 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   for (auto& x : sim) x.slot.assign(chunk, 0.0);
   std::vector<std::vector<int>> queue(8);  // indices into `all_tiles`: region tiles first, then chunks
   std::vector<TileDesc> all_tiles(seq);
-  for (int x = 0; x < 8; ++x)
-    for (const TileDesc& td : region_tiles[x]) {
-      sim[x].add(tile_time(td));
-      queue[x].push_back((int)all_tiles.size());
-      all_tiles.push_back(td);
-    }
+  auto put_regions = [&]() {
+    for (int x = 0; x < 8; ++x)
+      for (const TileDesc& td : region_tiles[x]) {
+        sim[x].add(tile_time(td));
+        queue[x].push_back((int)all_tiles.size());
+        all_tiles.push_back(td);
+      }
+  };
+  if (!regions_last) put_regions();
   const int TS = (int)seq.size();
   const char* tc_env = getenv("MXMOE_GG_TAIL_CHUNK");  // A/B switch: tail chunk size (default 16)
   const int tail_chunk = tc_env && atoi(tc_env) > 0 ? atoi(tc_env) : 16;
@@ -639,7 +647,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   for (int s0 = 0, c = 0; s0 < TS; ++c) {
     const bool head = TS - s0 > 16 * chunk;
     int len = (round_robin || head) ? chunk : std::min(chunk, tail_chunk);
-    if (head && !round_robin && regions_on) {
+    if (head && !round_robin && align_on) {
       // whole problems per chunk: split the rest of this problem's run into near-equal chunks of
       // about `chunk` tiles (a 33-tile expert stays on one XCD instead of spilling 1 tile onto
       // another that re-fetches its A rows), at most 64
@@ -672,6 +680,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     }
     s0 = s1;
   }
+  if (regions_last) put_regions();
   size_t qmax = 0;
   for (const auto& q : queue) qmax = std::max(qmax, q.size());
   int grid = 0;

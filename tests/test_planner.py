@@ -1,7 +1,7 @@
 """CPU tests of the host tile planner (gg_api.hip:plan_host) through mxmoe_gg_plan_tiles: every
 output tile of every problem is planned exactly once (split-K slices partition its K stages), and
 the placement rules hold — the shared expert of a bs=8192 layer is cut into one rectangle per XCD at
-the head of that XCD's queue, and routed experts are not split across XCDs by chunk boundaries.
+the end (or, switched, the head) of that XCD's queue, and routed experts are not split across XCDs by chunk boundaries.
 (The reference's TileScheduler, tile_scheduler.cuh:5-50, walks problems in order on the device; the
 placement is ours and affects speed and HBM traffic only, never results.)
 """
@@ -101,7 +101,10 @@ def _xcd_queues(tiles):
     return q
 
 
-def test_shared_expert_one_rectangle_per_xcd(monkeypatch):
+@pytest.mark.parametrize("placement", ["tail", "head"])
+def test_shared_expert_one_rectangle_per_xcd(monkeypatch, placement):
+    if placement == "head":
+        monkeypatch.setenv("MXMOE_GG_REGION", "1")
     shapes = _layer(8192)["gate_up"]  # the shared expert is the last problem: 32 x 44 tiles
     tiles, rows, v = check_coverage(shapes, nat.default_variant())
     shared = len(shapes) - 1
@@ -110,7 +113,10 @@ def test_shared_expert_one_rectangle_per_xcd(monkeypatch):
         is_shared = [int(rows[t[0]]) == shared for t in q[x]]
         n = sum(is_shared)
         assert n == 32 * 44 // 8
-        assert all(is_shared[:n]) and not any(is_shared[n:]), "region tiles must head the XCD queue"
+        if placement == "tail":  # the region closes the XCD's queue (default)
+            assert all(is_shared[-n:]) and not any(is_shared[:-n]), "region tiles must close the XCD queue"
+        else:
+            assert all(is_shared[:n]) and not any(is_shared[n:]), "region tiles must head the XCD queue"
         st = np.array([t for t, s in zip(q[x], is_shared) if s])
         m_panels, n_panels = len(np.unique(st[:, 1])), len(np.unique(st[:, 2]))
         # a rectangle: every (m, n) pair of its rows x columns
@@ -120,7 +126,14 @@ def test_shared_expert_one_rectangle_per_xcd(monkeypatch):
     monkeypatch.setenv("MXMOE_GG_REGION", "0")
     tiles0, rows0 = nat.plan_tiles(_probs(shapes), v)
     q0 = _xcd_queues(tiles0)
-    assert any(int(rows0[q0[x][0][0]]) != shared for x in range(8))
+    assert any(int(rows0[q0[x][-1][0]]) != shared for x in range(8)) or \
+        any(int(rows0[q0[x][0][0]]) != shared for x in range(8))
+    homes = collections.defaultdict(set)
+    for b, t in enumerate(tiles0):
+        if t[0] >= 0 and int(rows0[t[0]]) == shared:
+            homes[(t[1], t[2])].add(b % 8)
+    m_per_xcd = [len({m for (m, n), xs in homes.items() if x in xs}) for x in range(8)]
+    assert max(m_per_xcd) > 8  # chunked: every XCD sees most of the m-bands
 
 
 def test_routed_experts_stay_on_one_xcd():

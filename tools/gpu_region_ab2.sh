@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU box: kbench A/B of the planner placement switches (regions head / tail / off, chunk alignment).
+set -o pipefail
+TAG=${1:-region2}
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/$TAG
+V="auto,auto@MXMOE_GG_REGION=0,auto@MXMOE_GG_REGION=2,auto@MXMOE_GG_ALIGN=0"
+for cg in "fp16 gate_up" "fp16 down" "w8a8 gate_up" "w8a8 down" "mixed gate_up"; do
+  set -- $cg
+  timeout -k 10 150 python tools/kbench.py --cfg $1 --gg $2 --variants "$V" --iters 48 --rounds 8 >> gpurun_out/$TAG/kbench.jsonl || exit 1
+done
+cat gpurun_out/$TAG/kbench.jsonl

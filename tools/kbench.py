@@ -22,6 +22,29 @@ from mxmoe_amd.harness import build_layer_inputs, time_launches  # noqa: E402
 from mxmoe_amd.workload import QShape, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload  # noqa: E402
 
 
+def padded(inp, pad):
+    """The same inputs with every A / B row `pad` bytes longer (lda / ldb; fp16 and packed-int
+    problems only): moves consecutive rows off a power-of-two stride."""
+    import dataclasses
+
+    from mxmoe_amd.harness import LayerInputs
+
+    probs = []
+    for p in inp.problems:
+        if p.q.is_weight_only:
+            probs.append(p)
+            continue
+        def pad_rows(t):
+            u = t.view(torch.uint8)
+            out = torch.zeros(u.shape[0], u.shape[1] + pad, dtype=torch.uint8, device=u.device)
+            out[:, :u.shape[1]] = u
+            return out.view(t.dtype), (u.shape[1] + pad) // 2
+        A, lda = pad_rows(p.A)
+        B, ldb = pad_rows(p.B)
+        probs.append(dataclasses.replace(p, A=A, B=B, lda=lda, ldb=ldb))
+    return LayerInputs(problems=probs, shapes=inp.shapes)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", default="w8a8")
@@ -32,6 +55,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5, help="round-robin rounds over the variants")
     ap.add_argument("--bs", type=int, default=8192, help="tokens (routed M_e scale with it)")
     ap.add_argument("--settle-s", type=float, default=1.0, help="seconds of load before timing")
+    ap.add_argument("--pads", default="0", help="comma list of extra bytes per A / B row (row stride padding); "
+                    "each pad gets its own input set, every variant runs on every set")
     ap.add_argument("--dense", default="", help="M,N,K: one dense problem (fp16 / w8a8 / w4a4) instead of the layer")
     args = ap.parse_args()
     kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
@@ -51,17 +76,20 @@ def main():
         shapes = shapes[-1:]
     elif args.only == "routed":
         shapes = shapes[:-1]
-    inp = build_layer_inputs(shapes)
+    base = build_layer_inputs(shapes)
+    inputs = [(pad, base if pad == 0 else padded(base, pad)) for pad in (int(x) for x in args.pads.split(","))]
+    inp = base
     ggs, labels = [], []
-    for spec in args.variants.split(","):  # "8", "auto", or "8@ENV=value" (planned with ENV set)
+    for pad, spec in ((pad, spec) for pad, _ in inputs for spec in args.variants.split(",")):
+        inp_p = dict(inputs)[pad]
         x, _, env = spec.partition("@")
         saved = {}
         if env:
             k, val = env.split("=", 1)
             saved[k] = os.environ.get(k)
             os.environ[k] = val
-        ggs.append(GroupGemm(inp.problems, variant=None if x == "auto" else int(x)))  # None: AUTO
-        labels.append(spec)
+        ggs.append(GroupGemm(inp_p.problems, variant=None if x == "auto" else int(x)))  # None: AUTO
+        labels.append(spec if pad == 0 else f"{spec}+pad{pad}")
         for k, old in saved.items():
             if old is None:
                 os.environ.pop(k)

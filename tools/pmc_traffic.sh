@@ -13,7 +13,7 @@ for cfg in "$@"; do
   for gg in gate_up down; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 240 rocprofv3 --pmc $ctr --output-format csv -d $OUT/${cfg}_${gg}_${ctr} -o run -- \
-        python3 tools/kbench.py --cfg $cfg --gg $gg --variants auto --iters 10 > $OUT/${cfg}_${gg}_${ctr}.log 2>&1 || exit $?
+        python3 tools/kbench.py --cfg $cfg --gg $gg --variants auto --iters 10 ${KB_ARGS} > $OUT/${cfg}_${gg}_${ctr}.log 2>&1 || exit $?
     done
   done
 done
