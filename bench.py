@@ -6,13 +6,15 @@ One "step" = one pass of the hot path over one batch: the layer's two fused Grou
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config fp16|w8a8|w4a4|mixed] [--variant V]
   (N > 1: launched by torch.distributed.run, one rank per GPU)
 
-Multi-GPU (strong scaling): with N ranks the SAME layer is split by dist.nslice_plan
-into (problem, N-slice) work items, LPT-assigned (the shared expert — half of each call's FLOPs — is
-N-split); every rank writes its C slices into one packed shard and the shards are all-gathered over
-RCCL / xGMI, the gate_up gather on a second stream while down computes. value = the layer's FLOPs /
-max-over-ranks time of K such steps. extras.strong_scaling carries T1, compute-only and serial
-(no-overlap) times and both speedups; extras.ep_weak_scaling the expert-parallel weak-scaling
-number (N x 8192 tokens, no collective).
+Multi-GPU (strong scaling, SURVEY.md §8e, north_star): with N ranks the SAME layer is split by
+expert (dist.ep_layer_plan): routed experts by index (LPT on gate_up + down FLOPs), the shared expert
+by token rows sized to even out the ranks; each rank runs gate_up and down for its share (the gate_up
+output is the down call's input and stays on its rank) and the layer's outputs — every rank's down C,
+packed into one shard — are all-gathered over RCCL / xGMI. value = the layer's FLOPs / max-over-ranks
+time of K such steps. extras.strong_scaling carries T1, compute-only and step times and both
+speedups; extras.strong_scaling_nslice the N-slice split that all-gathers both calls' C (gate_up
+gather overlapped with down); extras.ep_weak_scaling the expert-parallel weak-scaling number
+(N x 8192 tokens, no collective).
 """
 from __future__ import annotations
 
@@ -156,6 +158,70 @@ def strong_scaling_step(cfg: str, dev, world: int, rank: int, steps: int, warmup
             "tiles": {gg: calls[gg].part.total_tiles if calls[gg].part is not None else 0 for gg in calls}}
 
 
+def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int, coll_dev, variant=None,
+                  median_iters: int = 50) -> dict:
+    """The N > 1 headline: ONE layer (the N = 1 workload) split by expert over the ranks
+    (dist.EPLayerStep). Every rank holds the full inputs (same seeds), runs gate_up and down over its
+    row items, and the packed down outputs are all-gathered over RCCL / xGMI. Timed K steps between
+    barriers + synchronisations, max over ranks, for: the full layer on one GPU (T1, every rank), the
+    sharded compute only, and compute + all-gather (the step)."""
+    import torch.distributed as dist
+
+    from mxmoe_amd.dist import EPLayerStep
+    from mxmoe_amd.groupgemm import GroupGemm
+    from mxmoe_amd.harness import build_layer_inputs, time_launches
+
+    layer = full_layer(cfg)
+    inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down")) for gg in ("gate_up", "down")}
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn, k=steps, w=warmup):
+        for _ in range(w):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    full = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
+    t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)))
+    del full
+    step = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant,
+                       shared=CONFIGS[cfg].get("model") != "mixtral")
+    t_comp = timed(lambda: step.compute(stream))
+    t_step = timed(lambda: step(stream))
+    flops = float(inp["gate_up"].flops + inp["down"].flops)
+    none = {"mean_ms": 0.0, "median_ms": 0.0}
+    per = {"gate_up": time_launches(lambda: step.gu.launch(stream), warmup=3, iters=median_iters, stream=stream)
+           if step.gu is not None else none,
+           "down": time_launches(lambda: step.dn.launch(stream), warmup=3, iters=median_iters, stream=stream)
+           if step.dn is not None else none}
+
+    def nbytes(shapes, w):
+        s = shapes[w.problem]
+        bits_a = 16 if s.a_bits == 16 else s.a_bits
+        return w.rows * s.N * 2 + w.rows * s.K * bits_a // 8 + s.N * s.K * s.w_bits // 8
+
+    mine = step.plan[rank]
+    gg_of = {"gate_up": step.gu, "down": step.dn}
+    return {"dt": t_step, "total_flops": flops, "t1": t1, "t_compute": t_comp, "per": per,
+            "flops_local": step.flops_local,
+            "bytes_local": {"gate_up": sum(nbytes(step.shapes_gu, w) for w in mine),
+                            "down": sum(nbytes(step.shapes_dn, w) for w in mine)},
+            "allgather_MB_received_per_rank": round(2 * step.pad * (world - 1) / 1e6, 1),
+            "items": len(mine),
+            "variant": (step.gu or step.dn).variant,
+            "tiles": {gg: g.total_tiles if g is not None else 0 for gg, g in gg_of.items()}}
+
+
 def cpu_info() -> dict:
     """Host CPU model and the threads the baseline may use (the GPU box exports OMP_NUM_THREADS=16:
     its share of a much larger machine, which os.cpu_count() would report)."""
@@ -267,7 +333,7 @@ def main():
                     help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
     ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 strong-scaling + all-gather extra")
+    ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 N-slice strong-scaling extra")
     ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
     args = ap.parse_args()
@@ -351,26 +417,40 @@ def main():
         f_gu, f_dn = main_res["flops"]["gate_up"], main_res["flops"]["down"]
         b_step = main_res["bytes"]["gate_up"] + main_res["bytes"]["down"]
     else:
-        # strong scaling of ONE layer over the node (the verdict's N > 1 headline): value = the
-        # layer's FLOPs / max-rank time of compute + RCCL all-gathers (gate_up gather overlapped)
-        sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev,
-                                   variant=args.variant if args.variant >= 0 else None, median_iters=args.median_iters)
-        main_res = {"dt": sres["dt"], "total_flops": sres["total_flops"], "per": sres["per"],
-                    "flops": sres["flops_local"], "variant": sres["variant"], "tiles": sres["tiles"],
+        # strong scaling of ONE layer over the node, split by expert (north_star): value = the
+        # layer's FLOPs / max-rank time of compute + the RCCL all-gather of the layer's outputs
+        vv = args.variant if args.variant >= 0 else None
+        eres = ep_layer_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
+                             median_iters=args.median_iters)
+        main_res = {"dt": eres["dt"], "total_flops": eres["total_flops"], "per": eres["per"],
+                    "flops": eres["flops_local"], "variant": eres["variant"], "tiles": eres["tiles"],
                     "shapes": full_layer(cfg)}
-        f_gu, f_dn = sres["flops_local"]["gate_up"], sres["flops_local"]["down"]
-        b_step = sres["bytes_local"]["gate_up"] + sres["bytes_local"]["down"]
+        f_gu, f_dn = eres["flops_local"]["gate_up"], eres["flops_local"]["down"]
+        b_step = eres["bytes_local"]["gate_up"] + eres["bytes_local"]["down"]
         ms = lambda t: t / args.steps * 1e3  # noqa: E731
         extras["strong_scaling"] = {
-            "what": "one layer split by dist.nslice_plan over the ranks; T1 = the whole layer on one GPU (max over "
-                    "ranks), compute = max-rank time of the local work lists, step = compute + RCCL "
-                    "all_gather_into_tensor of the packed C shards with the gate_up gather on a second stream "
-                    "beside the down call (value), serial = the same without the overlap",
-            "t1_ms": round(ms(sres["t1"]), 4), "compute_ms": round(ms(sres["t_compute"]), 4),
-            "step_ms": round(ms(sres["dt"]), 4), "serial_ms": round(ms(sres["t_serial"]), 4),
-            "speedup_compute": round(sres["t1"] / sres["t_compute"], 3),
-            "speedup_with_allgather": round(sres["t1"] / sres["dt"], 3),
-            "allgather_MB_received_per_rank": sres["allgather_MB_per_rank"]}
+            "what": "one layer split by expert (dist.ep_layer_plan: routed experts by index, shared expert by token "
+                    "rows); T1 = the whole layer on one GPU (max over ranks), compute = max-rank time of the local "
+                    "gate_up + down calls, step = compute + RCCL all_gather_into_tensor of the packed down "
+                    "outputs (value)",
+            "t1_ms": round(ms(eres["t1"]), 4), "compute_ms": round(ms(eres["t_compute"]), 4),
+            "step_ms": round(ms(eres["dt"]), 4),
+            "speedup_compute": round(eres["t1"] / eres["t_compute"], 3),
+            "speedup_with_allgather": round(eres["t1"] / eres["dt"], 3),
+            "allgather_MB_received_per_rank": eres["allgather_MB_received_per_rank"]}
+        if not args.no_strong_scaling:
+            try:  # the N-slice split: both calls' C all-gathered (gate_up gather beside down)
+                sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
+                                           median_iters=10)
+                extras["strong_scaling_nslice"] = {
+                    "what": "one layer split by dist.nslice_plan; step = compute + all-gather of every call's C "
+                            "(gate_up gather on a second stream beside the down call), serial = without the overlap",
+                    "step_ms": round(ms(sres["dt"]), 4), "compute_ms": round(ms(sres["t_compute"]), 4),
+                    "serial_ms": round(ms(sres["t_serial"]), 4),
+                    "speedup_with_allgather": round(sres["t1"] / sres["dt"], 3),
+                    "allgather_MB_received_per_rank": sres["allgather_MB_per_rank"]}
+            except Exception as e:  # an extra must not lose the headline
+                extras["strong_scaling_nslice"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         try:  # the round-1 headline, kept as an extra: expert-parallel weak scaling, no collective
             ep = run_config(cfg, args.steps, args.warmup, True)
             extras["ep_weak_scaling"] = {
@@ -457,13 +537,13 @@ def main():
                     "quantised problems; routed M_e = " + ("reference's committed bs=8192 histogram"
                                                          if not (cfg.startswith("ds2") or "model" in CONFIGS[cfg]) else
                                                          "seeded multinomial (SURVEY.md 8d)"),
-            "config": {"workload": CONFIGS[cfg]["name"] + (f", one layer split over {world} GPUs (N-slices + RCCL "
-                                                          f"all-gather of C)" if world > 1 else ""),
+            "config": {"workload": CONFIGS[cfg]["name"] + (f", one layer split by expert over {world} GPUs (RCCL "
+                                                          f"all-gather of the layer outputs)" if world > 1 else ""),
                        "model": {"mixtral": "Mixtral-8x7B", "qwen2_moe_57b": "Qwen2-57B-A14B"}.get(
                            CONFIGS[cfg].get("model"),
                            "DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")
                        + " MoE GroupGEMMs", "global_batch": CONFIGS[cfg].get("bs", 8192),
-                       "seq_len": None, "parallelism": f"nslice{world}+allgather" if world > 1 else "single",
+                       "seq_len": None, "parallelism": f"ep{world}+allgather" if world > 1 else "single",
                        "problems_per_call": len(main_res["shapes"]["gate_up"]), "variant": main_res["variant"],
                        "variant_name": nat.list_variants()[main_res["variant"]].split()[1]},
             "roofline": {**roof,

@@ -1,17 +1,20 @@
 """Multi-GPU partitioning of the GroupGEMM; one process per GPU, torch.distributed.
 
-The reference has no multi-GPU path (no NCCL/MPI call site); this module adds two:
+The reference has no multi-GPU path (no NCCL/MPI call site); this module adds three:
 
-* expert-parallel weak scaling (``ep_shard``) — what bench.py measures at N > 1: the global batch is
-  N x T tokens, routed experts are sharded by index over ranks (LPT on their FLOPs), each rank runs
-  its experts with N x M_e rows plus the replicated shared expert on its local T tokens. No
-  collective inside the GroupGEMM (dispatch/combine all-to-all belongs to the MoE layer).
-* strong scaling of one layer (``nslice_plan`` + ``ShardedCall`` + ``ShardedLayerStep``) — what
-  bench.py measures at N > 1: work items are (problem, N-slice) with slices a multiple of the tile
-  width, assigned by LPT; the shared expert (50 % of the FLOPs of each call) is N-split so the
-  speedup is not capped at 2x; every rank writes its C slices packed into one padded local shard and
-  the shards are exchanged with one all_gather_into_tensor per call over RCCL (xGMI). The gate_up
-  gather runs on a second stream while the down call computes.
+* expert-parallel strong scaling of one layer (``ep_layer_plan`` + ``EPLayerStep``) — bench.py's
+  N > 1 headline, north_star's "experts shard by index across the GPUs with an RCCL all-gather of
+  per-shard outputs": routed experts are sharded by index (LPT on their gate_up + down FLOPs), the
+  shared expert by token rows (sized so every rank's FLOPs even out); each rank runs gate_up and
+  down for its share — the gate_up output is the down call's input in the layer and stays on its
+  rank — and the layer's outputs (down C, packed into one shard per rank) are exchanged with one
+  all_gather_into_tensor over RCCL / xGMI.
+* strong scaling by N-slices (``nslice_plan`` + ``ShardedCall`` + ``ShardedLayerStep``) — an extra:
+  work items are (problem, N-slice) of each call; every call's C (gate_up included) is all-gathered,
+  the gate_up gather on a second stream while the down call computes.
+* expert-parallel weak scaling (``ep_shard``) — an extra: the global batch is N x T tokens, routed
+  experts are sharded by index, each rank runs its experts with N x M_e rows plus the replicated
+  shared expert on its local T tokens; no collective (dispatch / combine belongs to the MoE layer).
 """
 from __future__ import annotations
 
@@ -206,3 +209,122 @@ class ShardedLayerStep:
             self.dn.compute(stream)
             with torch.cuda.stream(stream):
                 self.dn.gather()
+
+
+@dataclasses.dataclass(frozen=True)
+class RowItem:
+    """Rows [m0, m1) of one problem (a whole routed expert, or a row slice of the shared expert)."""
+
+    problem: int
+    m0: int
+    m1: int
+
+    @property
+    def rows(self) -> int:
+        return self.m1 - self.m0
+
+
+def ep_layer_plan(gate_up: Sequence[QShape], down: Sequence[QShape], world: int, shared: bool = True,
+                  row_align: int = 64) -> list[list[RowItem]]:
+    """Per-rank work of one layer split by expert (the same items for the gate_up and down calls).
+
+    Routed experts (every problem but the last when ``shared``) go whole to ranks by LPT on their
+    gate_up + down FLOPs; the shared expert's token rows are cut into one contiguous slice per rank
+    (multiples of ``row_align`` rows, the last slice takes the rest) sized to fill each rank up to
+    an even share of the layer's FLOPs."""
+    P = len(gate_up)
+    nr = P - 1 if shared else P
+    routed = [i for i in range(nr) if gate_up[i].M > 0]
+    cost = [float(gate_up[i].flops + down[i].flops) for i in routed]
+    owner = lpt_assign(cost, world)
+    load = [0.0] * world
+    work: list[list[RowItem]] = [[] for _ in range(world)]
+    for i, o, c in zip(routed, owner, cost):
+        work[o].append(RowItem(i, 0, gate_up[i].M))
+        load[o] += c
+    if shared and P and gate_up[-1].M > 0:
+        M = gate_up[-1].M
+        per_row = float(gate_up[-1].flops + down[-1].flops) / M
+        target = (sum(load) + per_row * M) / world
+        want = [max(0.0, (target - ld) / per_row) for ld in load]
+        tot = sum(want)
+        want = [w * M / tot for w in want] if tot > 0 else [M / world] * world
+        bounds, acc = [0], 0.0
+        for r in range(world):
+            acc += want[r]
+            b = M if r == world - 1 else min(M, int(round(acc / row_align)) * row_align)
+            bounds.append(max(b, bounds[-1]))
+        for r in range(world):
+            if bounds[r + 1] > bounds[r]:
+                work[r].append(RowItem(P - 1, bounds[r], bounds[r + 1]))
+    return work
+
+
+def ep_shard_elems(shapes: Sequence[QShape], work: Sequence[RowItem]) -> int:
+    """fp16 output elements of one call that a rank's row items produce."""
+    return sum(w.rows * shapes[w.problem].N for w in work)
+
+
+def ep_scatter(shapes: Sequence[QShape], plan: list[list[RowItem]], gathered: torch.Tensor, pad: int,
+               outputs: Sequence[torch.Tensor]) -> None:
+    """Place an all-gathered buffer (rank r's packed shard at r * pad, items in work order, each a
+    [rows, N] row-major block) into the full per-problem outputs."""
+    for r, items in enumerate(plan):
+        off = r * pad
+        for w in items:
+            n = w.rows * shapes[w.problem].N
+            outputs[w.problem][w.m0:w.m1] = gathered[off:off + n].view(w.rows, shapes[w.problem].N)
+            off += n
+
+
+class EPLayerStep:
+    """This rank's part of one layer split by ``ep_layer_plan``: one planned gate_up call and one
+    down call over its row items, then one all_gather_into_tensor of the packed down outputs.
+
+    gate_up C is written into the full-size C tensors (rows of this rank's items only: it feeds the
+    down call of the same rank in the layer); down C goes into a packed local shard so the exchange
+    moves one contiguous buffer per rank."""
+
+    def __init__(self, gate_up, down, world: int, rank: int, variant: Optional[int] = None, group=None,
+                 shared: bool = True):
+        from .groupgemm import GroupGemm
+        from .harness import slice_rows
+
+        self.shapes_gu, self.shapes_dn = list(gate_up.shapes), list(down.shapes)
+        self.world, self.rank, self.group = world, rank, group
+        self.plan = ep_layer_plan(self.shapes_gu, self.shapes_dn, world, shared)
+        self.sizes = [ep_shard_elems(self.shapes_dn, w) for w in self.plan]
+        self.pad = max(max(self.sizes), 1)
+        dev = down.problems[0].C.device
+        self.local = torch.zeros(self.pad, dtype=torch.float16, device=dev)
+        self.gathered = torch.empty(world * self.pad, dtype=torch.float16, device=dev)
+        mine = self.plan[rank]
+        gu = [slice_rows(gate_up.problems[w.problem], w.m0, w.m1) for w in mine]
+        dn, off = [], 0
+        for w in mine:
+            p = down.problems[w.problem]
+            n = w.rows * p.N
+            dn.append(slice_rows(p, w.m0, w.m1, C=self.local[off:off + n].view(w.rows, p.N)))
+            off += n
+        self.gu = GroupGemm(gu, variant=variant, device=dev) if gu else None
+        self.dn = GroupGemm(dn, variant=variant, device=dev) if dn else None
+        self.flops_local = {"gate_up": sum(2 * w.rows * self.shapes_gu[w.problem].N * self.shapes_gu[w.problem].K
+                                           for w in mine),
+                            "down": sum(2 * w.rows * self.shapes_dn[w.problem].N * self.shapes_dn[w.problem].K
+                                        for w in mine)}
+
+    def compute(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        for gg in (self.gu, self.dn):
+            if gg is not None:
+                gg.launch(stream)
+
+    def gather(self) -> None:
+        _all_gather(self.gathered, self.local, self.group)
+
+    def __call__(self, stream: torch.cuda.Stream) -> None:
+        self.compute(stream)
+        with torch.cuda.stream(stream):
+            self.gather()
+
+    def scatter(self, outputs: Sequence[torch.Tensor]) -> None:
+        ep_scatter(self.shapes_dn, self.plan, self.gathered, self.pad, outputs)

@@ -139,6 +139,17 @@ def slice_problem(p: Problem, n0: int, n1: int) -> Problem:
                                scale_b=slice_scale_b(p, n0, n1))
 
 
+def slice_rows(p: Problem, m0: int, m1: int, C: Optional[torch.Tensor] = None) -> Problem:
+    """Rows [m0, m1) of a problem (tokens): A rows (a view), C rows (a view, or `C`), scale_a per
+    row — per-channel [M] -> a view, grouped [G][M] (w4a4 g128) -> a contiguous copy of [:, m0:m1]."""
+    sa = p.scale_a
+    if sa is not None:
+        G = 1 if p.q.gsize == -1 else p.K // p.q.gsize
+        sa = sa[m0:m1] if G == 1 else sa.reshape(G, p.M)[:, m0:m1].contiguous().reshape(-1)
+    return dataclasses.replace(p, A=p.A[m0:m1], C=p.C[m0:m1] if C is None else C, M=m1 - m0, scale_a=sa,
+                               ldc=0 if C is not None else p.ldc)
+
+
 def strong_scaling_sim(inputs: LayerInputs, worlds: Sequence[int] = (2, 4, 8), warmup: int = 5,
                        iters: int = 20, variant: Optional[int] = None) -> dict:
     """Compute-only strong scaling of one GroupGEMM call, measured on ONE GPU:

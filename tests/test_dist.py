@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mxmoe_amd.dist import allgather_outputs, ep_shard, lpt_assign, nslice_plan
+from mxmoe_amd.dist import allgather_outputs, ep_layer_plan, ep_scatter, ep_shard, ep_shard_elems, lpt_assign, nslice_plan
 from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
 
 
@@ -162,3 +162,96 @@ def test_nslice_layer_reassembles_oracle_output_gloo(world):
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res)
     assert all(split >= 2 for *_, split in res)  # the largest problem really was N-split across ranks
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("model", ["qwen2", "ds2", "mixtral"])
+def test_ep_layer_plan_covers_layer_and_balances(world, model):
+    from mxmoe_amd.workload import model_workload
+
+    if model == "qwen2":
+        layer = _layer()
+    else:
+        layer = next(iter(load_workload(model_workload(model, 8192)).values()))
+    gu, dn = layer["gate_up"], layer["down"]
+    shared = model != "mixtral"
+    plan = ep_layer_plan(gu, dn, world, shared=shared)
+    rows = {}
+    for items in plan:
+        for w in items:
+            rows.setdefault(w.problem, []).append((w.m0, w.m1))
+    for i, s in enumerate(gu):
+        if s.M == 0:
+            assert i not in rows
+            continue
+        spans = sorted(rows[i])
+        assert spans[0][0] == 0 and spans[-1][1] == s.M and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        if not (shared and i == len(gu) - 1):
+            assert len(spans) == 1  # a routed expert is never split: its gate_up output stays on its rank
+        else:
+            assert all(m0 % 64 == 0 for m0, _ in spans)
+    loads = [sum(w.rows * (gu[w.problem].N * gu[w.problem].K + dn[w.problem].N * dn[w.problem].K) for w in items)
+             for items in plan]
+    if shared:  # the shared expert's rows even out the routed experts' LPT remainder
+        assert max(loads) / (sum(loads) / world) < 1.03
+    assert sum(ep_shard_elems(dn, items) for items in plan) == sum(s.M * s.N for s in dn)
+
+
+def _ep_worker(rank, world, port, q):
+    """Each rank computes the down outputs of its ep_layer_plan row items with the oracle, packs them
+    in work order, all-gathers, scatters, and checks the whole layer output against the oracle's
+    full-problem C (bit-exact: a row slice does not change any output element's arithmetic)."""
+    import numpy as np
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        from tests._util import HostProblem
+        from mxmoe_amd.groupgemm import FP16, W4A4, W8A8
+        from mxmoe_amd.workload import QShape
+
+        specs = [(37, 256, 128, W8A8), (5, 256, 256, W4A4), (70, 128, 128, W8A8), (0, 256, 128, W4A4),
+                 (19, 256, 64, FP16), (640, 256, 256, W4A4)]  # last one: the shared expert, row-split
+        hps = [HostProblem(M, N, K, qq, seed=700 + i, device="cpu") for i, (M, N, K, qq) in enumerate(specs)]
+        shapes = [QShape([h.M, h.N, h.K], h.q.w_bits, h.q.a_bits, h.q.gsize, h.q.sym) for h in hps]
+        plan = ep_layer_plan(shapes, shapes, world)
+        pad = max(ep_shard_elems(shapes, w) for w in plan)
+        parts = []
+        for w in plan[rank]:
+            h = hps[w.problem]
+            K = h.K
+            if h.q.is_quant:
+                c = oracle.gg_quant(h.A[w.m0:w.m1], h.B, h.sa[w.m0:w.m1], h.sb, w.rows, h.N, K, h.q.a_bits)
+            else:
+                c = oracle.gg_f16(h.A[w.m0:w.m1], h.B, w.rows, h.N, K)
+            parts.append(torch.from_numpy(np.ascontiguousarray(c)).reshape(-1))
+        local = torch.zeros(pad, dtype=torch.float16)
+        if parts:
+            cat = torch.cat(parts)
+            local[:cat.numel()] = cat
+        gathered = torch.empty(world * pad, dtype=torch.float16)
+        dist.all_gather_into_tensor(gathered, local)
+        outs = [torch.full((max(s.M, 1), s.N), float("nan"), dtype=torch.float16) for s in shapes]
+        ep_scatter(shapes, plan, gathered, pad, outs)
+        ok = all(np.array_equal(outs[i][: h.M].numpy().view(np.uint16), h.expected().view(np.uint16))
+                 for i, h in enumerate(hps) if h.M)
+        split = sum(1 for items in plan for w in items if w.problem == 5)
+        q.put((rank, ok, split))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_ep_layer_reassembles_oracle_output_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ep_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(split == world for *_, split in res)  # the shared expert's rows were split over the ranks

@@ -1,5 +1,6 @@
-"""The N > 1 bench path on the GPU: dist.ShardedCall / ShardedLayerStep with 2 ranks sharing the one
-GPU of the box (gloo collectives staged through host memory; the node runs use RCCL). The gathered,
+"""The N > 1 bench paths on the GPU: dist.EPLayerStep (the headline: split by expert, down outputs
+all-gathered) and dist.ShardedCall / ShardedLayerStep (N-slices), with 2 ranks sharing the one GPU of
+the box (gloo collectives staged through host memory; the node runs use RCCL). The gathered,
 scattered layer output must equal one full single-GPU call (bit-exact on the integer paths)."""
 from __future__ import annotations
 
@@ -73,3 +74,66 @@ def test_sharded_layer_step_matches_full_call(cfg):
     for p in ps:
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
+
+
+def _ep_worker(rank, world, port, cfg, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import numpy as np
+
+        from mxmoe_amd.dist import EPLayerStep
+        from mxmoe_amd.groupgemm import GroupGemm
+        from mxmoe_amd.harness import build_layer_inputs
+        from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        kw = {"fp16": {}, "mixed": dict(qconfig=mixed_qconfig_lp1()), "w4a4_g128": dict(qstr="w4a4_g128_sym"),
+              "w4a16": dict(qstr="w4a16_g128_asym")}[cfg]
+        layer = load_workload(qwen2_layer11_workload(1024, **kw))["layer-11"]
+        inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=7 + (gg == "down")) for gg in ("gate_up", "down")}
+        step = EPLayerStep(inp["gate_up"], inp["down"], world, rank)
+        s = torch.cuda.current_stream(dev)
+        for p in inp["gate_up"].problems:
+            p.C.fill_(float("nan"))
+        step(s)
+        torch.cuda.synchronize(dev)
+        ok = True
+        outs = [torch.full_like(p.C, float("nan")) for p in inp["down"].problems]
+        step.scatter(outs)
+        gu_mine = [(p.C[w.m0:w.m1].clone(), w) for w in step.plan[rank] for p in [inp["gate_up"].problems[w.problem]]]
+        for gg in inp:
+            GroupGemm(inp[gg].problems).launch(s)  # the reference: one full call on this GPU
+        torch.cuda.synchronize(dev)
+
+        def same(a, b, quant):
+            a, b = a.cpu().numpy(), b.cpu().numpy()
+            if quant:
+                return bool(np.array_equal(a.view(np.uint16), b.view(np.uint16)))
+            return bool(np.allclose(a.astype(np.float64), b.astype(np.float64), rtol=2e-3, atol=2e-3))
+
+        for p, o in zip(inp["down"].problems, outs):  # the whole layer output, on every rank
+            ok &= same(o[: p.M], p.C[: p.M], p.q.is_quant and not p.q.is_weight_only)
+        for c, w in gu_mine:  # this rank's gate_up rows (they stay local)
+            p = inp["gate_up"].problems[w.problem]
+            ok &= same(c, p.C[w.m0:w.m1], p.q.is_quant and not p.q.is_weight_only)
+        q.put((rank, ok, len(step.plan[rank])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", ["mixed", "fp16", "w4a4_g128", "w4a16"])
+def test_ep_layer_step_matches_full_call(cfg):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ep_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(n > 0 for *_, n in res)
