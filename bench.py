@@ -497,18 +497,20 @@ def main():
                          "variant": r["variant"]}
 
     if world == 1 and not args.no_scaling_sim:
-        from mxmoe_amd.harness import build_layer_inputs as _bli, strong_scaling_sim, time_reference_abi
+        from mxmoe_amd.harness import build_layer_inputs as _bli, ep_scaling_sim, time_reference_abi
 
-        sim, asref = {}, {}
+        asref = {}
+        li = {gg: _bli(main_res["shapes"][gg], device=dev, seed=42 + (gg == "down")) for gg in ("gate_up", "down")}
+        sim = ep_scaling_sim(li["gate_up"], li["down"], variant=args.variant if args.variant >= 0 else None,
+                             shared=CONFIGS[cfg].get("model") != "mixtral")
         for gg in ("gate_up", "down"):
-            li = _bli(main_res["shapes"][gg], device=dev, seed=42 + (gg == "down"))
-            sim[gg] = strong_scaling_sim(li)
-            asref[gg] = round(time_reference_abi(li), 4)
-            del li
-            torch.cuda.empty_cache()
+            asref[gg] = round(time_reference_abi(li[gg]), 4)
+        del li
+        torch.cuda.empty_cache()
         extras["strong_scaling_sim"] = {
-            "what": "compute-only T1 / max-rank T_G of dist.nslice_plan work lists, each timed on this one GPU "
-                    "(ranks are independent GPUs); C all-gather not included (bytes per rank listed)",
+            "what": "compute-only T1 / max-rank T_G of the N > 1 headline's plan (dist.ep_layer_plan: gate_up + down "
+                    "per rank), each rank timed on this one GPU (ranks are independent GPUs); the all-gather of "
+                    "the down outputs is not included (MB received per rank listed)",
             **sim}
         f = main_res["flops"]
         extras["as_reference"] = {

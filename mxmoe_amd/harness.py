@@ -150,6 +150,33 @@ def slice_rows(p: Problem, m0: int, m1: int, C: Optional[torch.Tensor] = None) -
                                ldc=0 if C is not None else p.ldc)
 
 
+def ep_scaling_sim(gate_up: LayerInputs, down: LayerInputs, worlds: Sequence[int] = (2, 4, 8), warmup: int = 5,
+                   iters: int = 20, variant: Optional[int] = None, shared: bool = True) -> dict:
+    """Compute-only strong scaling of one layer split by expert (dist.ep_layer_plan, the N > 1
+    headline's plan), measured on ONE GPU: every rank's gate_up + down calls over its row items are
+    timed as their own calls (ranks are independent GPUs); T_G = max over ranks, speedup = T_1 / T_G.
+    The all-gather of the down outputs that follows on a node is listed as MB received per rank."""
+    from .dist import ep_layer_plan, ep_shard_elems
+
+    def t_pair(gu, dn):
+        ggs = [GroupGemm(x, variant=variant) for x in (gu, dn) if x]
+        return time_launches(lambda: [g.launch() for g in ggs], warmup, iters)["median_ms"]
+
+    t1 = t_pair(gate_up.problems, down.problems)
+    out = {"t1_ms": round(t1, 4)}
+    for G in worlds:
+        plan = ep_layer_plan(gate_up.shapes, down.shapes, G, shared)
+        rank_ms = [t_pair([slice_rows(gate_up.problems[w.problem], w.m0, w.m1) for w in items],
+                          [slice_rows(down.problems[w.problem], w.m0, w.m1) for w in items]) if items else 0.0
+                   for items in plan]
+        tg = max(rank_ms)
+        pad = max(ep_shard_elems(down.shapes, items) for items in plan)
+        out[str(G)] = {"t_ms_max_rank": round(tg, 4), "speedup": round(t1 / tg, 3),
+                       "rank_ms": [round(x, 4) for x in rank_ms],
+                       "allgather_MB_per_rank": round(2 * pad * (G - 1) / 1e6, 1)}
+    return out
+
+
 def strong_scaling_sim(inputs: LayerInputs, worlds: Sequence[int] = (2, 4, 8), warmup: int = 5,
                        iters: int = 20, variant: Optional[int] = None) -> dict:
     """Compute-only strong scaling of one GroupGEMM call, measured on ONE GPU:
