@@ -327,7 +327,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
+    # the chip needs ~0.2 s of sustained load to reach its steady clock: 10 warm-up steps read 3-5 %
+    # low on the headline and 5-8 % on the extras (profiles/r02/verify2/warmup_ab.jsonl)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="fp16", choices=list(CONFIGS))
     ap.add_argument("--no-scaling-sim", action="store_true",
                     help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
@@ -336,6 +338,7 @@ def main():
     ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 N-slice strong-scaling extra")
     ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
+    ap.add_argument("--extras-warmup", type=int, default=200, help="untimed steps before an extra config's launch timing")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -486,7 +489,7 @@ def main():
                           "roof_tflops": round(min(peak, f / b * HBM_GBS / 1e3), 1)}
     if world == 1 and args.extras:
         for x in [e for e in args.extras.split(",") if e and e != cfg]:
-            r = run_config(x, 0, 3, False)
+            r = run_config(x, 0, args.extras_warmup, False)
             pk = PEAK_TFLOPS[CONFIGS[x]["peak"]]
             tt = r["per"]["gate_up"]["median_ms"] + r["per"]["down"]["median_ms"]
             ff = r["flops"]["gate_up"] + r["flops"]["down"]
