@@ -198,6 +198,12 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
                        shared=CONFIGS[cfg].get("model") != "mixtral")
     t_comp = timed(lambda: step.compute(stream))
     t_step = timed(lambda: step(stream))
+    # the same split in 2 chunks per rank: chunk 0's gather on a second stream beside chunk 1's calls
+    step2 = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant,
+                        shared=CONFIGS[cfg].get("model") != "mixtral", chunks=2)
+    t_step2 = timed(lambda: step2(stream))
+    t_comp2 = timed(lambda: step2.compute(stream))
+    del step2
     flops = float(inp["gate_up"].flops + inp["down"].flops)
     none = {"mean_ms": 0.0, "median_ms": 0.0}
     per = {"gate_up": time_launches(lambda: step.gu.launch(stream), warmup=3, iters=median_iters, stream=stream)
@@ -213,6 +219,7 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
     mine = step.plan[rank]
     gg_of = {"gate_up": step.gu, "down": step.dn}
     return {"dt": t_step, "total_flops": flops, "t1": t1, "t_compute": t_comp, "per": per,
+            "t_step_chunked": t_step2, "t_compute_chunked": t_comp2,
             "flops_local": step.flops_local,
             "bytes_local": {"gate_up": sum(nbytes(step.shapes_gu, w) for w in mine),
                             "down": sum(nbytes(step.shapes_dn, w) for w in mine)},
@@ -441,6 +448,11 @@ def main():
             "speedup_compute": round(eres["t1"] / eres["t_compute"], 3),
             "speedup_with_allgather": round(eres["t1"] / eres["dt"], 3),
             "allgather_MB_received_per_rank": eres["allgather_MB_received_per_rank"]}
+        extras["strong_scaling_overlap"] = {
+            "what": "the same expert split, each rank's work in 2 chunks: chunk 0's all-gather on a second stream "
+                    "beside chunk 1's gate_up + down calls",
+            "step_ms": round(ms(eres["t_step_chunked"]), 4), "compute_ms": round(ms(eres["t_compute_chunked"]), 4),
+            "speedup_with_allgather": round(eres["t1"] / eres["t_step_chunked"], 3)}
         if not args.no_strong_scaling:
             try:  # the N-slice split: both calls' C all-gathered (gate_up gather beside down)
                 sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,

@@ -277,54 +277,107 @@ def ep_scatter(shapes: Sequence[QShape], plan: list[list[RowItem]], gathered: to
             off += n
 
 
+def ep_layer_chunks(plan: list[list[RowItem]], gate_up: Sequence[QShape], down: Sequence[QShape], chunks: int,
+                    row_align: int = 64) -> list[list[list[RowItem]]]:
+    """Cut every rank's work into `chunks` groups of about equal FLOPs (a shared-expert row slice is
+    cut into `chunks` row parts first, in multiples of `row_align`; then LPT): returns one per-rank
+    plan per chunk, so that chunk c's outputs can be all-gathered while chunk c + 1 computes."""
+    if chunks <= 1:
+        return [plan]
+    out: list[list[list[RowItem]]] = [[[] for _ in plan] for _ in range(chunks)]
+    for r, items in enumerate(plan):
+        pieces = []
+        for w in items:
+            if w.rows >= chunks * row_align and w.problem == len(gate_up) - 1:
+                step = -(-w.rows // chunks // row_align) * row_align
+                pieces += [RowItem(w.problem, m, min(w.m1, m + step)) for m in range(w.m0, w.m1, step)]
+            else:
+                pieces.append(w)
+        cost = [float(w.rows) * (gate_up[w.problem].N * gate_up[w.problem].K + down[w.problem].N * down[w.problem].K)
+                for w in pieces]
+        for w, c in zip(pieces, lpt_assign(cost, chunks)):
+            out[c][r].append(w)
+    return out
+
+
 class EPLayerStep:
-    """This rank's part of one layer split by ``ep_layer_plan``: one planned gate_up call and one
-    down call over its row items, then one all_gather_into_tensor of the packed down outputs.
+    """This rank's part of one layer split by ``ep_layer_plan``: per chunk (``ep_layer_chunks``) one
+    planned gate_up call and one down call over its row items, and one all_gather_into_tensor of
+    the chunk's packed down outputs. With chunks > 1 the gather of chunk c runs on a second stream
+    while chunk c + 1 computes (RCCL runs the gathers in issue order on that stream).
 
     gate_up C is written into the full-size C tensors (rows of this rank's items only: it feeds the
     down call of the same rank in the layer); down C goes into a packed local shard so the exchange
-    moves one contiguous buffer per rank."""
+    moves one contiguous buffer per rank and chunk."""
 
     def __init__(self, gate_up, down, world: int, rank: int, variant: Optional[int] = None, group=None,
-                 shared: bool = True):
+                 shared: bool = True, chunks: int = 1):
         from .groupgemm import GroupGemm
         from .harness import slice_rows
 
         self.shapes_gu, self.shapes_dn = list(gate_up.shapes), list(down.shapes)
         self.world, self.rank, self.group = world, rank, group
         self.plan = ep_layer_plan(self.shapes_gu, self.shapes_dn, world, shared)
-        self.sizes = [ep_shard_elems(self.shapes_dn, w) for w in self.plan]
-        self.pad = max(max(self.sizes), 1)
+        self.chunk_plans = ep_layer_chunks(self.plan, self.shapes_gu, self.shapes_dn, chunks)
         dev = down.problems[0].C.device
-        self.local = torch.zeros(self.pad, dtype=torch.float16, device=dev)
-        self.gathered = torch.empty(world * self.pad, dtype=torch.float16, device=dev)
+        self.parts = []  # per chunk: (gate_up call, down call, local shard, gathered, pad)
+        for cplan in self.chunk_plans:
+            pad = max(max(ep_shard_elems(self.shapes_dn, w) for w in cplan), 1)
+            local = torch.zeros(pad, dtype=torch.float16, device=dev)
+            gathered = torch.empty(world * pad, dtype=torch.float16, device=dev)
+            mine = cplan[rank]
+            gu = [slice_rows(gate_up.problems[w.problem], w.m0, w.m1) for w in mine]
+            dn, off = [], 0
+            for w in mine:
+                p = down.problems[w.problem]
+                n = w.rows * p.N
+                dn.append(slice_rows(p, w.m0, w.m1, C=local[off:off + n].view(w.rows, p.N)))
+                off += n
+            self.parts.append((GroupGemm(gu, variant=variant, device=dev) if gu else None,
+                               GroupGemm(dn, variant=variant, device=dev) if dn else None, local, gathered, pad))
+        self.pad = sum(p[4] for p in self.parts)
         mine = self.plan[rank]
-        gu = [slice_rows(gate_up.problems[w.problem], w.m0, w.m1) for w in mine]
-        dn, off = [], 0
-        for w in mine:
-            p = down.problems[w.problem]
-            n = w.rows * p.N
-            dn.append(slice_rows(p, w.m0, w.m1, C=self.local[off:off + n].view(w.rows, p.N)))
-            off += n
-        self.gu = GroupGemm(gu, variant=variant, device=dev) if gu else None
-        self.dn = GroupGemm(dn, variant=variant, device=dev) if dn else None
         self.flops_local = {"gate_up": sum(2 * w.rows * self.shapes_gu[w.problem].N * self.shapes_gu[w.problem].K
                                            for w in mine),
                             "down": sum(2 * w.rows * self.shapes_dn[w.problem].N * self.shapes_dn[w.problem].K
                                         for w in mine)}
+        self.comm = torch.cuda.Stream(device=dev) if dev.type == "cuda" and len(self.parts) > 1 else None
+        self.evs = [torch.cuda.Event() for _ in self.parts] if self.comm is not None else []
+
+    @property
+    def gu(self):
+        return self.parts[0][0]
+
+    @property
+    def dn(self):
+        return self.parts[0][1]
 
     def compute(self, stream: Optional[torch.cuda.Stream] = None) -> None:
-        for gg in (self.gu, self.dn):
-            if gg is not None:
-                gg.launch(stream)
+        for gu, dn, *_ in self.parts:
+            for gg in (gu, dn):
+                if gg is not None:
+                    gg.launch(stream)
 
     def gather(self) -> None:
-        _all_gather(self.gathered, self.local, self.group)
+        for *_, local, gathered, _pad in self.parts:
+            _all_gather(gathered, local, self.group)
 
     def __call__(self, stream: torch.cuda.Stream) -> None:
-        self.compute(stream)
-        with torch.cuda.stream(stream):
-            self.gather()
+        if self.comm is None:
+            self.compute(stream)
+            with torch.cuda.stream(stream):
+                self.gather()
+            return
+        for (gu, dn, local, gathered, _pad), ev in zip(self.parts, self.evs):
+            for gg in (gu, dn):
+                if gg is not None:
+                    gg.launch(stream)
+            ev.record(stream)
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                _all_gather(gathered, local, self.group)
+        stream.wait_stream(self.comm)
 
     def scatter(self, outputs: Sequence[torch.Tensor]) -> None:
-        ep_scatter(self.shapes_dn, self.plan, self.gathered, self.pad, outputs)
+        for cplan, (*_, gathered, pad) in zip(self.chunk_plans, self.parts):
+            ep_scatter(self.shapes_dn, cplan, gathered, pad, outputs)

@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mxmoe_amd.dist import allgather_outputs, ep_layer_plan, ep_scatter, ep_shard, ep_shard_elems, lpt_assign, nslice_plan
+from mxmoe_amd.dist import allgather_outputs, ep_layer_chunks, ep_layer_plan, ep_scatter, ep_shard, ep_shard_elems, lpt_assign, nslice_plan
 from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
 
 
@@ -255,3 +255,25 @@ def test_ep_layer_reassembles_oracle_output_gloo(world):
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert all(split == world for *_, split in res)  # the shared expert's rows were split over the ranks
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 3])
+def test_ep_layer_chunks_partition_each_rank(chunks):
+    layer = _layer()
+    gu, dn = layer["gate_up"], layer["down"]
+    plan = ep_layer_plan(gu, dn, 8)
+    cps = ep_layer_chunks(plan, gu, dn, chunks)
+    assert len(cps) == chunks
+    for r, items in enumerate(plan):
+        rows = {}
+        for cp in cps:
+            for w in cp[r]:
+                rows.setdefault(w.problem, []).append((w.m0, w.m1))
+        assert sorted(rows) == sorted(w.problem for w in items)
+        for w in items:
+            spans = sorted(rows[w.problem])
+            assert spans[0][0] == w.m0 and spans[-1][1] == w.m1 and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        if chunks > 1:
+            loads = [sum(w.rows * (gu[w.problem].N * gu[w.problem].K + dn[w.problem].N * dn[w.problem].K) for w in cp[r])
+                     for cp in cps]
+            assert max(loads) < 1.35 * sum(loads) / chunks

@@ -76,7 +76,7 @@ def test_sharded_layer_step_matches_full_call(cfg):
     assert all(ok for _, ok, _ in res), res
 
 
-def _ep_worker(rank, world, port, cfg, q):
+def _ep_worker(rank, world, port, cfg, q, chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -93,7 +93,7 @@ def _ep_worker(rank, world, port, cfg, q):
               "w4a16": dict(qstr="w4a16_g128_asym")}[cfg]
         layer = load_workload(qwen2_layer11_workload(1024, **kw))["layer-11"]
         inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=7 + (gg == "down")) for gg in ("gate_up", "down")}
-        step = EPLayerStep(inp["gate_up"], inp["down"], world, rank)
+        step = EPLayerStep(inp["gate_up"], inp["down"], world, rank, chunks=chunks)
         s = torch.cuda.current_stream(dev)
         for p in inp["gate_up"].problems:
             p.C.fill_(float("nan"))
@@ -123,13 +123,13 @@ def _ep_worker(rank, world, port, cfg, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg", ["mixed", "fp16", "w4a4_g128", "w4a16"])
-def test_ep_layer_step_matches_full_call(cfg):
+@pytest.mark.parametrize("cfg,chunks", [("mixed", 1), ("fp16", 1), ("w4a4_g128", 1), ("w4a16", 1), ("mixed", 2)])
+def test_ep_layer_step_matches_full_call(cfg, chunks):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_ep_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    ps = [ctx.Process(target=_ep_worker, args=(r, world, port, cfg, q, chunks)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
