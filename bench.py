@@ -345,6 +345,7 @@ def main():
     ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 N-slice strong-scaling extra")
     ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
+    ap.add_argument("--dist-extras", default="ds2_mixed", help="other configs run through the expert split at N > 1")
     ap.add_argument("--extras-warmup", type=int, default=200, help="untimed steps before an extra config's launch timing")
     args = ap.parse_args()
 
@@ -453,6 +454,21 @@ def main():
                     "beside chunk 1's gate_up + down calls",
             "step_ms": round(ms(eres["t_step_chunked"]), 4), "compute_ms": round(ms(eres["t_compute_chunked"]), 4),
             "speedup_with_allgather": round(eres["t1"] / eres["t_step_chunked"], 3)}
+        for x in [e for e in args.dist_extras.split(",") if e and e != cfg]:
+            try:  # BASELINE configs[4]: DeepSeek-V2-Lite mixed w4a4+w8a8 split by expert over the node
+                xr = ep_layer_step(x, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
+                                   median_iters=10)
+                extras[x + "_ep"] = {
+                    "what": CONFIGS[x]["name"] + f", one layer split by expert over {world} GPUs + RCCL all-gather "
+                                                 "of the layer outputs",
+                    "tflops": round(xr["total_flops"] * args.steps / xr["dt"] / 1e12, 3),
+                    "step_ms": round(ms(xr["dt"]), 4), "t1_ms": round(ms(xr["t1"]), 4),
+                    "compute_ms": round(ms(xr["t_compute"]), 4),
+                    "speedup_compute": round(xr["t1"] / xr["t_compute"], 3),
+                    "speedup_with_allgather": round(xr["t1"] / xr["dt"], 3),
+                    "chunked_step_ms": round(ms(xr["t_step_chunked"]), 4)}
+            except Exception as e:  # an extra must not lose the headline
+                extras[x + "_ep"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if not args.no_strong_scaling:
             try:  # the N-slice split: both calls' C all-gathered (gate_up gather beside down)
                 sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
