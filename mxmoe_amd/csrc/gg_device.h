@@ -477,6 +477,26 @@ __device__ __forceinline__ void wait_vmcnt() {
 // LDS barrier that lets LDS-DMA stay in flight: drain this wave's LDS reads, barrier, and keep the
 // compiler from moving LDS accesses across it (the "memory" clobbers) — unlike __syncthreads(),
 // no vmcnt(0).
+// One 16-B row chunk of C at `base` + `off` elements, `base` wave-uniform (the wave's first output
+// row / column). C is written once and never read back by the kernel, so the store carries sc1,
+// which drops the line from the XCD's L2 (plain stores keep it, MI355X_MICROARCH.md "stores of each
+// flavour") and leaves L2 to the A / B panels: a buffer store, base in SGPRs, 32-bit byte offset per
+// lane — `narrow` (wave-uniform) says every offset of the wave fits, else a plain 64-bit store.
+// Measured (profiles/r02/region/sc1_*): counter bytes -8 % on the w8a8 step, -1.4 % fp16, time
+// unchanged. -DMXMOE_STORE_PLAIN builds the plain stores for A/B.
+__device__ __forceinline__ void store_c16(_Float16* base, int64_t off, bool narrow, const uint4& v) {
+#ifndef MXMOE_STORE_PLAIN
+  if (narrow) {
+    typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+    const v4u_ d = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(d, __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000),
+                                           (int)(off * 2), 0, 16 /* sc1 */);
+    return;
+  }
+#endif
+  *reinterpret_cast<uint4*>(base + off) = v;
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -963,6 +983,8 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
     }
   }
+  _Float16* const cbase = C + (int64_t)mrow0 * mt.ldc + ncol0;  // wave-uniform
+  const bool narrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;  // byte offsets < 2^30
   // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
 #pragma unroll 4
   for (int it = 0; it < Cfg::WTM / 8; ++it) {
@@ -972,7 +994,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     if constexpr ((ABL & ABL_NO_EPI) != 0) {
       asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
     } else {
-      if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+      if (m < M && n < N) store_c16(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
     }
   }
 }
@@ -1190,12 +1212,14 @@ __device__ __forceinline__ void gg_tile_g128(const GGMeta& mt, const uint8_t* __
       *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (eg & 1) * 8) = pk;
     }
   }
+  _Float16* const cbase = C + (int64_t)mrow0 * mt.ldc + ncol0;  // wave-uniform
+  const bool narrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;  // byte offsets < 2^30
 #pragma unroll 4
   for (int it = 0; it < Cfg::WTM / 8; ++it) {
     const int row = it * 8 + (elane >> 3), q = elane & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
     const int m = mrow0 + row, n = ncol0 + q * 8;
-    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+    if (m < M && n < N) store_c16(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
   }
 }
 
@@ -1272,12 +1296,14 @@ __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>:
     }
   }
   constexpr int RPI = 64 / CPR;  // staged rows per wave-instruction
+  _Float16* const cbase = C + (int64_t)mrow0 * mt.ldc + ncol0;  // wave-uniform
+  const bool narrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;  // byte offsets < 2^30
 #pragma unroll 4
   for (int it = 0; it < Cfg::WTM / RPI; ++it) {
     const int row = it * RPI + lane / CPR, q = lane % CPR;
     const uint4 v = *reinterpret_cast<const uint4*>(reg + row * RB + ((q ^ (row & (CPR - 1))) << 4));
     const int m = mrow0 + row, n = ncol0 + q * 8;
-    if (m < M && n < N) *reinterpret_cast<uint4*>(C + (int64_t)m * mt.ldc + n) = v;
+    if (m < M && n < N) store_c16(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
   }
 }
 
