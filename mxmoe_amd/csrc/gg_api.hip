@@ -967,6 +967,15 @@ struct ShimDev {
   size_t ws_cap = 0;
   uint8_t* pinned = nullptr;
   size_t pin_cap = 0;
+  // plan cache: the last call's shapes / quant params (key), its plan, and the pointer columns the
+  // workspace holds. A call with the same key skips planning and the tile-table upload (a caller
+  // runs the same layer shapes call after call); new pointers re-upload the columns only.
+  bool cached = false;
+  std::vector<int64_t> key;
+  Plan plan;
+  int variant = -1;
+  WsLayout layout{};
+  std::vector<const void*> cols;  // 5 x P, plan order, as in the workspace
 };
 std::mutex g_shim_mu;
 std::vector<ShimDev> g_shim;  // indexed by device ordinal
@@ -1047,7 +1056,40 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
                         (int)h_problem_sizes[i].y, (int)h_problem_sizes[i].z, h_qbits_list[i].a_bits,
                         h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0,
                         h_qbits_list[i].fmt};
-  // 2. plan with the same NULL / alignment checks as mxmoe_gg_plan (a bad pointer is an error code,
+  // 2. same shapes as the last call on this device: reuse its plan (the pointers still get the same
+  //    NULL / alignment checks as mxmoe_gg_plan)
+  std::vector<int64_t> key;
+  key.reserve((size_t)problem_count * 8);
+  for (const HostProblem& p : hp)
+    key.insert(key.end(), {p.M, p.N, p.K, p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt});
+  if (d.cached && key == d.key) {
+    const Variant& v = variants()[d.variant];
+    std::vector<const void*> cols;
+    cols.reserve(5 * d.plan.order.size());
+    for (int c = 0; c < 5; ++c)
+      for (int r : d.plan.order) {
+        GGMeta m;
+        if (c == 0) {
+          st = build_meta(hp[r], r, v, true, &m);
+          if (st) return st;
+        }
+        const HostProblem& q = hp[r];
+        cols.push_back(c == 0 ? q.A : c == 1 ? q.B : c == 2 ? q.SA : c == 3 ? q.SB : q.C);
+      }
+    if (cols != d.cols) {  // new buffers, same shapes: upload the 5 pointer columns only
+      const size_t P = d.plan.order.size();
+      std::memset(d.pinned, 0, 5 * d.layout.ptr);
+      for (int c = 0; c < 5; ++c) memcpy(d.pinned + c * d.layout.ptr, cols.data() + c * P, P * sizeof(void*));
+      HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(d.ws) + d.layout.meta, d.pinned, 5 * d.layout.ptr,
+                             hipMemcpyHostToDevice, nullptr));
+      d.cols = std::move(cols);
+    }
+    mxmoe_gg_plan_info info;
+    fill_info(d.plan, d.variant, d.layout, d.ws, &info);
+    return mxmoe_gg_launch(&info, nullptr);
+  }
+  d.cached = false;
+  // 3. plan with the same NULL / alignment checks as mxmoe_gg_plan (a bad pointer is an error code,
   //    never a fault inside the LDS-DMA kernel)
   int variant;
   st = resolve_variant(MXMOE_GG_VARIANT_AUTO, hp, &variant);
@@ -1066,15 +1108,24 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
   }
   WsLayout l;
   std::vector<uint8_t> img = workspace_image(plan, cols, &l);
-  // 3. upload from pinned memory and launch, both on the legacy stream, no further host sync: the
+  // 4. upload from pinned memory and launch, both on the legacy stream, no further host sync: the
   //    next shim call on this device synchronises that stream before it rewrites either buffer
-  st = shim_grow(d, l.total, std::max(5 * col, img.size()));
+  st = shim_grow(d, l.total, std::max(std::max(5 * col, img.size()), 5 * l.ptr));
   if (st) return st;
   memcpy(d.pinned, img.data(), img.size());
   HIP_TRY(hipMemcpyAsync(d.ws, d.pinned, img.size(), hipMemcpyHostToDevice, nullptr));
   mxmoe_gg_plan_info info;
   fill_info(plan, variant, l, d.ws, &info);
-  return mxmoe_gg_launch(&info, nullptr);
+  st = mxmoe_gg_launch(&info, nullptr);
+  if (st) return st;
+  d.key = std::move(key);
+  d.variant = variant;
+  d.layout = l;
+  d.cols.clear();
+  for (int c = 0; c < 5; ++c) d.cols.insert(d.cols.end(), cols[c].begin(), cols[c].end());
+  d.plan = std::move(plan);
+  d.cached = true;
+  return MXMOE_GG_OK;
 }
 
 

@@ -262,3 +262,30 @@ def test_reference_abi_shim_rejects_null_scale():
     hps[0].problem.scale_b = None  # the gathered pointer is NULL: an error code, not a GPU fault
     with pytest.raises(nat.GGError, match="NULL scale"):
         _shim_call(hps)
+
+
+def test_reference_abi_shim_plan_cache():
+    """Same shapes call after call reuse the cached plan: with the same buffers (nothing uploaded),
+    with new buffers (pointer columns re-uploaded), and a NULL scale still fails on a cache hit."""
+    specs = [(300, 256, 512, W8A8), (65, 256, 512, W4A4), (20, 128, 128, FP16), (0, 128, 128, W8A8)]
+    a = [HostProblem(M, N, K, q, seed=90 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
+    b = [HostProblem(M, N, K, q, seed=190 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
+    _shim_call(a)  # plans and caches
+    torch.cuda.synchronize()
+    _check(a)
+    for h in a:
+        h.problem.C.fill_(float("nan"))
+    _shim_call(a)  # cache hit, same pointers
+    torch.cuda.synchronize()
+    _check(a)
+    _shim_call(b)  # cache hit, new pointers
+    torch.cuda.synchronize()
+    _check(b)
+    for h in a:
+        h.problem.C.fill_(float("nan"))
+    _shim_call(a)  # and back
+    torch.cuda.synchronize()
+    _check(a)
+    b[0].problem.scale_a = None
+    with pytest.raises(nat.GGError, match="NULL scale"):
+        _shim_call(b)
