@@ -545,7 +545,8 @@ def main():
             **sim}
         f = main_res["flops"]
         extras["as_reference"] = {
-            "what": "groupgemm_mxmoe (reference FuncType): per-call host plan + table upload + launch, wall ms",
+            "what": "groupgemm_mxmoe (reference FuncType) called back to back: per call the D2H pointer gather + one "
+                    "sync, the plan (cached per device for repeated shapes; pointers re-validated) and the launch, wall ms",
             "gate_up_ms": asref["gate_up"], "down_ms": asref["down"],
             "tflops": round((f["gate_up"] + f["down"]) / ((asref["gate_up"] + asref["down"]) * 1e-3) / 1e12, 2)}
 
