@@ -524,6 +524,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   const char* region_env = getenv("MXMOE_GG_REGION");  // A/B switch: 0 off, 1 queue head, 2 tail (default)
   const bool regions_on = !(region_env && region_env[0] == '0');
   const bool regions_last = !(region_env && region_env[0] == '1');
+  const char* rot_env = getenv("MXMOE_GG_REGION_ROT");  // A/B switch (default off)
+  const bool region_rot = rot_env && rot_env[0] == '1';
   const char* align_env = getenv("MXMOE_GG_ALIGN");  // A/B switch: problem-aligned chunks (default on)
   const bool align_on = !(align_env && align_env[0] == '0');
   struct Region {
@@ -573,14 +575,23 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
         auto put = [&](int mi, int n) {
           region_tiles[x].push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second, 0, nst, -1, -1});
         };
+        // (MXMOE_GG_REGION_ROT: XCD x starts its sweep x/8 of the way along the swept axis, so the
+        // XCDs do not all stream the same panels at the same time)
+        const int span_n = nb1 - nb0, span_m = mb1 - mb0;
+        const int rot_n = region_rot && span_n > 0 ? (x * span_n / 8) : 0;
+        const int rot_m = region_rot && span_m > 0 ? (x * span_m / 8) : 0;
         if (rg.nband) {
           for (int nb = nb0; nb < nb1; nb += (int)band)
-            for (int mi = mb0; mi < mb1; ++mi)
+            for (int k = 0; k < span_m; ++k) {
+              const int mi = mb0 + (k + rot_m) % span_m;
               for (int n = nb; n < std::min(nb1, nb + (int)band); ++n) put(mi, n);
+            }
         } else {
           for (int mb = mb0; mb < mb1; mb += (int)band)
-            for (int n = nb0; n < nb1; ++n)
+            for (int k = 0; k < span_n; ++k) {
+              const int n = nb0 + (k + rot_n) % span_n;
               for (int mi = mb; mi < std::min(mb1, mb + (int)band); ++mi) put(mi, n);
+            }
         }
       }
       plan->meta.push_back(m);
