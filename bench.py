@@ -30,6 +30,10 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+# The reference's published GroupGEMM TFLOPS (RTX-4090, read off media/final-perf.png by eye, about
+# +-5 %) — context only: BASELINE.json publishes no number, so vs_baseline stays null.
+REFERENCE_CHART_TFLOPS = {"fp16": 145.0, "w8a8": 420.0, "w4a4": 690.0, "mixed": 545.0, "ds2_mixed": 578.0}
+
 PEAK_TFLOPS = {"fp16": 2500.0, "int8": 5000.0, "fp8": 5000.0}  # dense MFMA peaks, MI355X_MICROARCH.md (spec)
 HBM_GBS = 8000.0
 
@@ -549,6 +553,14 @@ def main():
                     "sync, the plan (cached per device for repeated shapes; pointers re-validated) and the launch, wall ms",
             "gate_up_ms": asref["gate_up"], "down_ms": asref["down"],
             "tflops": round((f["gate_up"] + f["down"]) / ((asref["gate_up"] + asref["down"]) * 1e-3) / 1e12, 2)}
+
+    if world == 1:
+        ref = {"hardware": "RTX-4090", "source": "reference README media/final-perf.png read by eye (BASELINE.md §1)"}
+        for c in [cfg] + [x for x in args.extras.split(",") if x in extras]:
+            if c in REFERENCE_CHART_TFLOPS:
+                mine = value if c == cfg else extras[c]["tflops"]
+                ref[c] = {"reference_tflops": REFERENCE_CHART_TFLOPS[c], "ratio": round(mine / REFERENCE_CHART_TFLOPS[c], 2)}
+        extras["reference_published_chart"] = ref
 
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
