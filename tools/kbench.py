@@ -64,12 +64,16 @@ def main():
           "w4a16c": dict(qstr="w4a16_g-1_sym"), "w8a16": dict(qstr="w8a16_g-1_asym"),
           "w4a16ga": dict(qstr="w4a16_g-1_asym"), "w4a16gs": dict(qstr="w4a16_g128_sym"),
           "w4a4g128": dict(qstr="w4a4_g128_sym"), "w2a16": dict(qstr="w2a16_g128_asym"),
-          "e4m3": dict(qstr="w8a8_g-1_sym_E4M3"), "bf16": dict(qstr="bf16")}[args.cfg]
+          "e4m3": dict(qstr="w8a8_g-1_sym_E4M3"), "bf16": dict(qstr="bf16"), "ds2_mixed": {}}[args.cfg]
     if args.dense:
         bits = {"fp16": 16, "w8a8": 8, "w4a4": 4, "e4m3": 8, "bf16": 16}[args.cfg]
         fmt = {"e4m3": "E4M3", "bf16": "bf16"}.get(args.cfg, "")
         shapes = [QShape([int(x) for x in args.dense.split(",")], bits, bits, fmt=fmt)]
         args.gg = "dense_" + args.dense.replace(",", "x")
+    elif args.cfg == "ds2_mixed":
+        from mxmoe_amd.workload import ds2_mixed_qconfig, ds2_workload
+
+        shapes = load_workload(ds2_workload(args.bs, qconfig=ds2_mixed_qconfig()))["layer-1"][args.gg]
     else:
         shapes = load_workload(qwen2_layer11_workload(args.bs, **kw))["layer-11"][args.gg]
     if args.only == "shared":
