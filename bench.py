@@ -229,7 +229,7 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
                             "down": sum(nbytes(step.shapes_dn, w) for w in mine)},
             "allgather_MB_received_per_rank": round(2 * step.pad * (world - 1) / 1e6, 1),
             "items": len(mine),
-            "variant": (step.gu or step.dn).variant,
+            "variant": (step.gu or step.dn).variant if (step.gu or step.dn) is not None else -1,
             "tiles": {gg: g.total_tiles if g is not None else 0 for gg, g in gg_of.items()}}
 
 
