@@ -41,3 +41,23 @@ def test_slice_problem_scales_every_layout():
         assert s.scale_b.is_contiguous() and s.N == 256 and s.B.shape[0] == 256
         if q.is_quant and not q.is_weight_only:
             assert torch.equal(s.scale_a, p.scale_a)
+
+
+def test_slice_rows_scales_every_layout():
+    """harness.slice_rows (the expert split's shared-expert row slices): rows [m0, m1) of A, C and
+    the per-row scales — per-channel [M] as a view, w4a4 g128 [K/128][M] as a copy of [:, m0:m1]."""
+    from mxmoe_amd.harness import slice_rows
+
+    for q in QS:
+        hp = HostProblem(200, 128, 256, q, seed=12, device="cpu")
+        p = hp.problem
+        s = slice_rows(p, 64, 192)
+        assert s.M == 128 and torch.equal(s.A, p.A[64:192]) and s.C.data_ptr() == p.C[64:].data_ptr()
+        if p.scale_a is None:
+            assert s.scale_a is None
+            continue
+        G = 1 if q.gsize == -1 else 256 // q.gsize
+        assert torch.equal(s.scale_a.reshape(G, 128), p.scale_a.reshape(G, 200)[:, 64:192]), q.qcfg
+        assert s.scale_a.is_contiguous() and s.scale_b is p.scale_b
+        C = torch.zeros(128, 128, dtype=torch.float16)
+        assert slice_rows(p, 64, 192, C=C).C is C
