@@ -211,9 +211,6 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | ABL_WO_BTILED>("abl_v2s_wo_btiled"),
       make_v2<V2_STAGGER | ABL_WO_NODMA>("abl_v2s_wo_nodma"),
       make_v2<V2_STAGGER | ABL_WO_NOCOMPUTE>("abl_v2s_wo_nocompute"),
-      // staggered v2 / v2s3 with the early waves' A fragment reads pipelined two rows ahead
-      make_v2<V2_STAGGER | V2_PIPE>("v2sp_256x256_w8_dma_stagger_pipe"),
-      make_v2<V2_STAGGER | V2_B3 | V2_PIPE>("v2s3p_256x256_w8_dma_stagger_bring3_pipe"),
   };
   return v;
 }

@@ -562,7 +562,6 @@ enum : int {
   ABL_B_REGLOAD = 1024,  // ablation: B operand loaded into registers (same global traffic), not into LDS
   ABL_B_TILED = 2048,    // ablation: B read as if stored in contiguous 32-KiB (256 rows x 128 B) stage blocks
   V2_B3 = 4096,          // stagger: B in a 3-stage LDS ring, two stages ahead (A: 2 stages, one ahead)
-  V2_PIPE = 8192,        // stagger, early waves: A fragment reads software-pipelined two rows ahead
   // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
   // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
   ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
@@ -622,46 +621,6 @@ struct V2Half {
 #pragma unroll
       for (int j = 0; j < FN; ++j) b[t][j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
     }
-  }
-  // Early waves (V2_PIPE): read and multiply one half stage with the A fragment reads two rows
-  // ahead of their MFMAs. Left alone, hipcc reads A two rows at a time right before their 8 MFMAs
-  // (read, lgkmcnt(0), 8 MFMAs, ...): the LDS latency sits between every group. The group barriers
-  // below fix the order {B + A rows 0-3 reads}, {8 MFMAs}, {A rows 4-5}, {8 MFMAs}, {A rows 6-7},
-  // {16 MFMAs}, so each pair of reads lands under 8 MFMAs (+16 VGPRs in the early path only).
-  __device__ __forceinline__ void read_mma_pipe(const uint8_t* abase, const uint8_t* bbase, uint32_t a_row,
-                                                uint32_t b_row, int swz, int g, int h,
-                                                typename AccT<QT>::type (&acc)[FM][FN]) const {
-    static_assert(QT == QT_I8 || QT == QT_F16 || QT == QT_BF16, "V2_PIPE: 16-B fragment bodies only");
-    static_assert(FM == 8 && FN == 4, "V2_PIPE: 128 x 64 wave tiles");
-    const uint8_t* As = abase + a_row;
-    const uint8_t* Bs = bbase + b_row;
-    const uint32_t off = (uint32_t)(((h * 4 + g) ^ swz) << 4);
-    word_t bf[FN], af[FM];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const word_t*>(As + i * 2048 + off);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if constexpr (QT == QT_I8) {
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bf[j], af[i], acc[i][j], 0, 0, 0);
-        } else if constexpr (QT == QT_BF16) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, bf[j]),
-                                                              __builtin_bit_cast(v8bf, af[i]), acc[i][j], 0, 0, 0);
-        } else {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, bf[j]),
-                                                             __builtin_bit_cast(v8h, af[i]), acc[i][j], 0, 0, 0);
-        }
-      }
-    // masks: 0x100 DS read, 0x008 MFMA
-    __builtin_amdgcn_sched_group_barrier(0x100, FN + 4, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * FN, 0);
   }
   __device__ __forceinline__ void mma(typename AccT<QT>::type (&acc)[FM][FN]) const {
 #pragma unroll
@@ -928,15 +887,10 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         for (int s = 0; s < nst; ++s) {
           if (s + 1 < nst) issue_a(s + 1);
           if (s + 2 < nst) issue_b(s + 2);
-          if constexpr ((ABL & V2_PIPE) != 0 && QT != QT_I4 && QT != QT_F8 && Cfg::FM == 8 && Cfg::FN == 4) {
-            fr.read_mma_pipe(abuf(s), bbuf(s), a_row, b_row, swz, g, 0, acc);
-            fr.read_mma_pipe(abuf(s), bbuf(s), a_row, b_row, swz, g, 1, acc);
-          } else {
-            hread(fr, s, 0);
-            hmma(fr);
-            hread(fr, s, 1);
-            hmma(fr);
-          }
+          hread(fr, s, 0);
+          hmma(fr);
+          hread(fr, s, 1);
+          hmma(fr);
           sync_next(s);
         }
       }
@@ -968,16 +922,10 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       } else {
         for (int s = 0; s < nst; ++s) {
           if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
-          if constexpr ((ABL & V2_PIPE) != 0 && QT != QT_I4 && QT != QT_F8 && Cfg::FM == 8 && Cfg::FN == 4) {
-            const uint8_t* st = lds + (s & 1) * Cfg::STAGE_BYTES;
-            fr.read_mma_pipe(st, st + Cfg::A_BYTES, a_row, b_row, swz, g, 0, acc);
-            fr.read_mma_pipe(st, st + Cfg::A_BYTES, a_row, b_row, swz, g, 1, acc);
-          } else {
-            hread(fr, s & 1, 0);
-            hmma(fr);
-            hread(fr, s & 1, 1);
-            hmma(fr);
-          }
+          hread(fr, s & 1, 0);
+          hmma(fr);
+          hread(fr, s & 1, 1);
+          hmma(fr);
           stage_sync(s);
         }
       }
