@@ -85,16 +85,22 @@ def k_key(K: int) -> str:
 
 def runtime_cost(workloads, strategies: Sequence[str], table: dict, tiles: dict) -> list:
     """get_runtime_cost (bits_solver.py:518-542) on the MI355X table: cost[e][i][j] = inc * num_tiles
-    of problem i of expert e under strategy j. One compiled tile per strategy runs every strategy in
-    one launch, so there is no fusion enumeration (the reference's outer tile-combination axis).
-    ``workloads[e][i]`` has M, N, K; ``tiles[qcfg]`` is the TileConfig the table was measured with."""
+    of problem i of expert e under strategy j, with the inc of the nearest K class scaled by
+    K / K_class (a tile's mainloop is linear in K; the reference reads one fixed key per strategy
+    family, which misprices a K = 1408 down projection by 27 % against its 1024 class —
+    tests/test_perf_table_gpu.py checks the prediction against measured layer calls). One compiled
+    tile per strategy runs every strategy in one launch, so there is no fusion enumeration (the
+    reference's outer tile-combination axis). ``workloads[e][i]`` has M, N, K; ``tiles[qcfg]`` is
+    the TileConfig the table was measured with."""
     out = []
     for exp in workloads:
         row = []
         for w in exp:
-            row.append([table[q][k_key(w.K)][tile_repr(tiles[q], q)]["inc"] * num_tiles(w.M, w.N, tiles[q])
+            kk = k_key(w.K)
+            scale = w.K / (1024 * int(kk))
+            row.append([table[q][kk][tile_repr(tiles[q], q)]["inc"] * scale * num_tiles(w.M, w.N, tiles[q])
                         if q in table else
-                        table[ALIASES[q]][k_key(w.K)][tile_repr(tiles[ALIASES[q]], ALIASES[q])]["inc"] *
+                        table[ALIASES[q]][kk][tile_repr(tiles[ALIASES[q]], ALIASES[q])]["inc"] * scale *
                         num_tiles(w.M, w.N, tiles[ALIASES[q]])
                         for q in strategies])
         out.append(row)

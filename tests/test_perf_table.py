@@ -50,7 +50,7 @@ def test_runtime_cost_is_inc_times_tiles():
     tiles = {q: t for q in table}
     cost = pt.runtime_cost([[_P(300, 2816, 2048), _P(8192, 2048, 1408)]], ["w8a8_g-1_sym", "w4a4_g-1_sym"], table, tiles)
     assert cost[0][0] == [pytest.approx(0.002 * 2 * 11)] * 2  # K=2048 -> key "2"; 2 x 11 tiles
-    assert cost[0][1][0] == pytest.approx(0.001 * 32 * 8)      # K=1408 -> key "1"
+    assert cost[0][1][0] == pytest.approx(0.001 * 1408 / 1024 * 32 * 8)  # K=1408 -> key "1", scaled by K
     assert pt.tiles_from_table(table)["w8a8_g-1_sym"] == dataclasses.replace(t, MMA="MFMA_I8_K64")
 
 
