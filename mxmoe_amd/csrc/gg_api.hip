@@ -225,7 +225,6 @@ constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
 // fp16 / w8a8 down, routed problems +7-9 %; +-1 % on gate_up, -1..3 % on dense 8192^3)
 constexpr const char* kShortKVariant = "v2s3_256x256_w8_dma_stagger_bring3";
 constexpr int kShortKStages = 24;
-constexpr int kLowReuseMTiles = 4;  // <= 4 m-tiles (M <= 1024): a B panel serves at most one band
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
@@ -734,7 +733,6 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   } else if (mask & ((1 << QT_F16) | (1 << QT_I8) | (1 << QT_I4) | (1 << QT_F8) | (1 << QT_BF16))) {
     std::vector<std::pair<int, int64_t>> st;  // (128-B K stages, tiles) of the fp16 / w8a8 / w4a4 problems
     int64_t total = 0, f16_small = 0;         // f16_small: fp16 tiles of the 64-row class
-    int64_t low_reuse = 0;                    // tiles of problems with <= kLowReuseMTiles m-tiles
     for (const HostProblem& p : hp) {
       int qt;
       if (p.M <= 0 || qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt, &qt) != MXMOE_GG_OK) continue;
@@ -743,15 +741,10 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
       st.emplace_back((int)(((int64_t)p.K * p.a_bits / 8 + 127) / 128), tiles);
       total += tiles;
       if (is_float16(qt) && p.M % 256 > 0 && p.M % 256 <= 64) f16_small += nt;
-      if ((p.M + 255) / 256 <= kLowReuseMTiles) low_reuse += tiles;
     }
     // low-fill fp16 calls (most tiles are 64-row remainders, e.g. bs=512 routed experts): those
     // tiles wait on their B stream, and the deeper B ring pays (+5-9 %, session3/exp_b3_bs512.jsonl)
-    // calls whose tiles mostly belong to few-m-tile problems (routed experts): each B panel is
-    // streamed by only a few tiles, so it comes from beyond L2 and the deeper B ring pays at any K
-    // (fp16 gate_up routed problems +4.5-5 %, the shared expert alone -1.5 %, the whole call +1 %:
-    // profiles/r02/ab/kbench_shortk_reuse.jsonl)
-    if (total > 0 && (2 * f16_small >= total || 2 * low_reuse >= total)) {
+    if (total > 0 && 2 * f16_small >= total) {
       *out = variant_index(kShortKVariant);
       return MXMOE_GG_OK;
     }
