@@ -32,7 +32,8 @@ import torch  # noqa: E402
 
 # The reference's published GroupGEMM TFLOPS (RTX-4090, read off media/final-perf.png by eye, about
 # +-5 %) — context only: BASELINE.json publishes no number, so vs_baseline stays null.
-REFERENCE_CHART_TFLOPS = {"fp16": 145.0, "w8a8": 420.0, "w4a4": 690.0, "mixed": 545.0, "ds2_mixed": 578.0}
+REFERENCE_CHART_TFLOPS = {"fp16": 145.0, "w8a8": 420.0, "w4a4": 690.0, "mixed": 545.0, "ds2_mixed": 578.0,
+                          "w4a16_w8a8_bs512": 115.0}  # bs=512 W4.25A15.5 bar
 
 PEAK_TFLOPS = {"fp16": 2500.0, "int8": 5000.0, "fp8": 5000.0}  # dense MFMA peaks, MI355X_MICROARCH.md (spec)
 HBM_GBS = 8000.0
@@ -61,6 +62,11 @@ CONFIGS = {
                         name="qwen2_moe layer-11 w2a16_g128_asym GroupGEMM bs=512 (weight-bandwidth bound)"),
     "fp16_bs512": dict(kw={}, peak="fp16", dtype="fp16", bs=512,
                        name="qwen2_moe layer-11 fp16 GroupGEMM bs=512"),
+    # the reference's published small-batch mixed scheme (W4.25A15.5, README / SURVEY §6): w4a16_g-1_asym
+    # + w8a8_g-1_sym per linear block in one fused launch (hz_fused.cuh:14-125, ref_bind.cu:412)
+    "w4a16_w8a8_bs512": dict(kw="w4a16_w8a8", peak="fp16", dtype="fp16 (int4 weights) + int8", bs=512,
+                             name="qwen2_moe layer-11 mixed w4a16_g-1_asym + w8a8_g-1_sym (W4.25A15.5) GroupGEMM "
+                                  "bs=512 (weight-bandwidth bound)"),
     # the reference's other SUPPORTED_QCFG strategies (tile_config.py:40-106)
     "w8a8_e4m3": dict(kw=dict(qstr="w8a8_g-1_sym_E4M3"), peak="fp8", dtype="fp8 e4m3",
                       name="qwen2_moe layer-11 w8a8_g-1_sym_E4M3 GroupGEMM bs=8192 (fp8 MFMA, f32 accumulate)"),
@@ -102,6 +108,10 @@ def full_layer(cfg: str, bs: int = 8192):
         return load_workload(ds2_workload(bs, qconfig=ds2_mixed_qconfig()))["layer-1"]
     if kw == "mixed":
         kw = dict(qconfig=mixed_qconfig_lp1())
+    elif kw == "w4a16_w8a8":
+        from mxmoe_amd.workload import w4a16_w8a8_qconfig
+
+        kw = dict(qconfig=w4a16_w8a8_qconfig())
     return load_workload(qwen2_layer11_workload(bs, **kw))["layer-11"]
 
 
@@ -162,6 +172,11 @@ def strong_scaling_step(cfg: str, dev, world: int, rank: int, steps: int, warmup
             "tiles": {gg: calls[gg].part.total_tiles if calls[gg].part is not None else 0 for gg in calls}}
 
 
+def _gather_only(step, stream) -> None:
+    with torch.cuda.stream(stream):
+        step.gather()
+
+
 def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int, coll_dev, variant=None,
                   median_iters: int = 50) -> dict:
     """The N > 1 headline: ONE layer (the N = 1 workload) split by expert over the ranks
@@ -171,7 +186,7 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
     sharded compute only, and compute + all-gather (the step)."""
     import torch.distributed as dist
 
-    from mxmoe_amd.dist import EPLayerStep
+    from mxmoe_amd.dist import EPLayerStep, choose_chunks, gather_ms_model
     from mxmoe_amd.groupgemm import GroupGemm
     from mxmoe_amd.harness import build_layer_inputs, time_launches
 
@@ -198,16 +213,21 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
     full = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
     t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)))
     del full
-    step = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant,
-                       shared=CONFIGS[cfg].get("model") != "mixtral")
+    shared = CONFIGS[cfg].get("model") != "mixtral"
+    step = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant, shared=shared)
     t_comp = timed(lambda: step.compute(stream))
+    t_gather = timed(lambda: _gather_only(step, stream))
     t_step = timed(lambda: step(stream))
-    # the same split in 2 chunks per rank: chunk 0's gather on a second stream beside chunk 1's calls
-    step2 = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant,
-                        shared=CONFIGS[cfg].get("model") != "mixtral", chunks=2)
-    t_step2 = timed(lambda: step2(stream))
-    t_comp2 = timed(lambda: step2.compute(stream))
-    del step2
+    # the compute / all-gather pipeline depth: dist.choose_chunks on this node's measured compute and
+    # gather times (max over ranks), then the chosen split timed as the headline step
+    chunks = choose_chunks(t_comp / steps * 1e3, t_gather / steps * 1e3)
+    if chunks > 1:
+        stepc = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant, shared=shared, chunks=chunks)
+        t_stepc = timed(lambda: stepc(stream))
+        t_compc = timed(lambda: stepc.compute(stream))
+        del stepc
+    else:
+        t_stepc, t_compc = t_step, t_comp
     flops = float(inp["gate_up"].flops + inp["down"].flops)
     none = {"mean_ms": 0.0, "median_ms": 0.0}
     per = {"gate_up": time_launches(lambda: step.gu.launch(stream), warmup=3, iters=median_iters, stream=stream)
@@ -222,8 +242,9 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
 
     mine = step.plan[rank]
     gg_of = {"gate_up": step.gu, "down": step.dn}
-    return {"dt": t_step, "total_flops": flops, "t1": t1, "t_compute": t_comp, "per": per,
-            "t_step_chunked": t_step2, "t_compute_chunked": t_comp2,
+    return {"dt": t_stepc, "total_flops": flops, "t1": t1, "t_compute": t_comp, "per": per,
+            "chunks": chunks, "t_step_1chunk": t_step, "t_compute_chunked": t_compc, "t_gather": t_gather,
+            "gather_model_ms": gather_ms_model(2 * step.pad * (world - 1), world),
             "flops_local": step.flops_local,
             "bytes_local": {"gate_up": sum(nbytes(step.shapes_gu, w) for w in mine),
                             "down": sum(nbytes(step.shapes_dn, w) for w in mine)},
@@ -346,8 +367,10 @@ def main():
                     help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
     ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-strong-scaling", action="store_true", help="skip the N > 1 N-slice strong-scaling extra")
-    ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed", help="other configs measured as extra fields (N=1)")
+    ap.add_argument("--dist-extras-all", action="store_true",
+                    help="N > 1: also run the N-slice strong-scaling and EP weak-scaling extras (off by default: "
+                         "the default N > 1 run exercises one RCCL path, the expert split)")
+    ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed,w4a16_w8a8_bs512", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
     ap.add_argument("--dist-extras", default="ds2_mixed", help="other configs run through the expert split at N > 1")
     ap.add_argument("--extras-warmup", type=int, default=200, help="untimed steps before an extra config's launch timing")
@@ -446,18 +469,17 @@ def main():
         extras["strong_scaling"] = {
             "what": "one layer split by expert (dist.ep_layer_plan: routed experts by index, shared expert by token "
                     "rows); T1 = the whole layer on one GPU (max over ranks), compute = max-rank time of the local "
-                    "gate_up + down calls, step = compute + RCCL all_gather_into_tensor of the packed down "
-                    "outputs (value)",
+                    "gate_up + down calls, gather = the RCCL all_gather_into_tensor of the packed down outputs "
+                    "alone, step (value) = compute and gather pipelined in `chunks` chunks (dist.choose_chunks on "
+                    "the measured compute / gather times), step_1chunk = compute then gather",
             "t1_ms": round(ms(eres["t1"]), 4), "compute_ms": round(ms(eres["t_compute"]), 4),
-            "step_ms": round(ms(eres["dt"]), 4),
+            "gather_ms": round(ms(eres["t_gather"]), 4), "gather_model_ms": round(eres["gather_model_ms"], 4),
+            "chunks": eres["chunks"], "step_ms": round(ms(eres["dt"]), 4),
+            "step_1chunk_ms": round(ms(eres["t_step_1chunk"]), 4),
+            "compute_chunked_ms": round(ms(eres["t_compute_chunked"]), 4),
             "speedup_compute": round(eres["t1"] / eres["t_compute"], 3),
             "speedup_with_allgather": round(eres["t1"] / eres["dt"], 3),
             "allgather_MB_received_per_rank": eres["allgather_MB_received_per_rank"]}
-        extras["strong_scaling_overlap"] = {
-            "what": "the same expert split, each rank's work in 2 chunks: chunk 0's all-gather on a second stream "
-                    "beside chunk 1's gate_up + down calls",
-            "step_ms": round(ms(eres["t_step_chunked"]), 4), "compute_ms": round(ms(eres["t_compute_chunked"]), 4),
-            "speedup_with_allgather": round(eres["t1"] / eres["t_step_chunked"], 3)}
         for x in [e for e in args.dist_extras.split(",") if e and e != cfg]:
             try:  # BASELINE configs[4]: DeepSeek-V2-Lite mixed w4a4+w8a8 split by expert over the node
                 xr = ep_layer_step(x, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
@@ -469,11 +491,10 @@ def main():
                     "step_ms": round(ms(xr["dt"]), 4), "t1_ms": round(ms(xr["t1"]), 4),
                     "compute_ms": round(ms(xr["t_compute"]), 4),
                     "speedup_compute": round(xr["t1"] / xr["t_compute"], 3),
-                    "speedup_with_allgather": round(xr["t1"] / xr["dt"], 3),
-                    "chunked_step_ms": round(ms(xr["t_step_chunked"]), 4)}
+                    "speedup_with_allgather": round(xr["t1"] / xr["dt"], 3), "chunks": xr["chunks"]}
             except Exception as e:  # an extra must not lose the headline
                 extras[x + "_ep"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        if not args.no_strong_scaling:
+        if args.dist_extras_all:
             try:  # the N-slice split: both calls' C all-gathered (gate_up gather beside down)
                 sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
                                            median_iters=10)
@@ -486,15 +507,16 @@ def main():
                     "allgather_MB_received_per_rank": sres["allgather_MB_per_rank"]}
             except Exception as e:  # an extra must not lose the headline
                 extras["strong_scaling_nslice"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        try:  # the round-1 headline, kept as an extra: expert-parallel weak scaling, no collective
-            ep = run_config(cfg, args.steps, args.warmup, True)
-            extras["ep_weak_scaling"] = {
-                "what": "global batch N x 8192 tokens, routed experts sharded by index (LPT), shared expert "
-                        "replicated on local tokens; no collective (dispatch / combine is MoE plumbing)",
-                "value_tflops": round(ep["total_flops"] * args.steps / ep["dt"] / 1e12, 3),
-                "ms_per_step": round(ep["dt"] / args.steps * 1e3, 4)}
-        except Exception as e:  # an extra must not lose the headline
-            extras["ep_weak_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if args.dist_extras_all:
+            try:  # the round-1 headline, kept as an extra: expert-parallel weak scaling, no collective
+                ep = run_config(cfg, args.steps, args.warmup, True)
+                extras["ep_weak_scaling"] = {
+                    "what": "global batch N x 8192 tokens, routed experts sharded by index (LPT), shared expert "
+                            "replicated on local tokens; no collective (dispatch / combine is MoE plumbing)",
+                    "value_tflops": round(ep["total_flops"] * args.steps / ep["dt"] / 1e12, 3),
+                    "ms_per_step": round(ep["dt"] / args.steps * 1e3, 4)}
+            except Exception as e:  # an extra must not lose the headline
+                extras["ep_weak_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     per = main_res["per"]
     t_gu, t_dn = per["gate_up"]["mean_ms"], per["down"]["mean_ms"]
     achieved = (f_gu + f_dn) / ((t_gu + t_dn) * 1e-3) / 1e12
@@ -525,11 +547,17 @@ def main():
             pk = PEAK_TFLOPS[CONFIGS[x]["peak"]]
             tt = r["per"]["gate_up"]["median_ms"] + r["per"]["down"]["median_ms"]
             ff = r["flops"]["gate_up"] + r["flops"]["down"]
+            bb = r["bytes"]["gate_up"] + r["bytes"]["down"]
             extras[x] = {"tflops": round(ff / (tt * 1e-3) / 1e12, 2),
                          "gate_up_tflops": round(r["flops"]["gate_up"] / (r["per"]["gate_up"]["median_ms"] * 1e-3) / 1e12, 2),
                          "down_tflops": round(r["flops"]["down"] / (r["per"]["down"]["median_ms"] * 1e-3) / 1e12, 2),
-                         "roofline_frac": round(ff / (tt * 1e-3) / 1e12 / pk, 4), "peak_tflops": pk,
-                         "variant": r["variant"]}
+                         "ms_per_step": round(tt, 4), "variant": r["variant"]}
+            if ff / bb * HBM_GBS / 1e3 < pk:  # the HBM roof binds (small batches: the weight stream)
+                gbs = bb / (tt * 1e-3) / 1e9
+                extras[x].update(bound="hbm", roofline_frac=round(gbs / HBM_GBS, 4), achieved_gbs=round(gbs, 1),
+                                 algorithmic_MB=round(bb / 1e6, 1), peak_gbs=HBM_GBS)
+            else:
+                extras[x].update(bound="mfma", roofline_frac=round(ff / (tt * 1e-3) / 1e12 / pk, 4), peak_tflops=pk)
 
     if world == 1 and not args.no_scaling_sim:
         from mxmoe_amd.harness import build_layer_inputs as _bli, ep_scaling_sim, time_reference_abi

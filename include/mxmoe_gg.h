@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MXMOE_GG_ABI_VERSION 4
+#define MXMOE_GG_ABI_VERSION 5  /* 5: QParams padding ignored, groupgemm_mxmoe_fmt */
 
 enum {
   MXMOE_GG_OK = 0,
@@ -61,15 +61,15 @@ enum {
 
 /* Same memory layout as the reference's mxmoe::QParams (quantize.cuh:14-25):
  * int2 qbits {x = a_bits, y = w_bits}; int gsize; bool sym; padded to 16 bytes, 8-byte aligned.
- * `fmt` sits in the byte after `sym` that the reference leaves as padding, so a reference caller
- * that value-initialises its QParams passes MXMOE_GG_FMT_DEFAULT. */
+ * The three bytes after `sym` are the reference's padding: its QParams constructors
+ * (quantize.cuh:19-20) leave them uninitialised, so nothing in this library reads them. Operand
+ * formats other than the default travel in mxmoe_gg_problem.fmt or groupgemm_mxmoe_fmt's array. */
 typedef struct mxmoe_qparams {
   int32_t a_bits;
   int32_t w_bits;
   int32_t gsize;
   uint8_t sym;
-  uint8_t fmt;
-  uint8_t pad_[2];
+  uint8_t pad_[3];
 } __attribute__((aligned(8))) mxmoe_qparams;
 
 /* Same memory layout as CUDA/HIP dim3 (x = M, y = N, z = K), as used in registry.cuh:28-39. */
@@ -105,6 +105,7 @@ typedef struct mxmoe_gg_plan_info {
   int32_t splitk_slabs;    /* 256-KiB partial-sum slabs the plan's split-K tiles use (0: no split) */
   int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */
   void* workspace;         /* device workspace the plan was written to */
+  uint64_t signature;      /* hash of the plan table and tile table (shapes, quant params, strides) */
 } mxmoe_gg_plan_info;
 
 int mxmoe_gg_abi_version(void);
@@ -150,6 +151,12 @@ int mxmoe_gg_workspace_size(const mxmoe_gg_problem* problems, int problem_count,
 int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int variant, void* workspace,
                   size_t workspace_bytes, void* stream, mxmoe_gg_plan_info* info);
 
+/* Re-point a plan at new operand buffers: `problems` must describe the same shapes, quant params
+ * and strides as the planned call (checked through the plan signature, MXMOE_GG_ERR_INVALID
+ * otherwise); only the 5 pointer columns of the workspace are uploaded (one copy on `stream` and a
+ * stream synchronisation). The pointers get mxmoe_gg_plan's NULL / alignment checks. */
+int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const mxmoe_gg_plan_info* info, void* stream);
+
 /* Launch a planned GroupGEMM on `stream`. No allocation, no synchronisation. */
 int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream);
 
@@ -170,6 +177,14 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
                     void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
                     mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
                     mxmoe_qparams* h_qbits_list, int problem_count);
+
+/* groupgemm_mxmoe with an explicit operand format per problem (h_fmts[i] = MXMOE_GG_FMT_*, host
+ * array; NULL = MXMOE_GG_FMT_DEFAULT for every problem, i.e. exactly groupgemm_mxmoe). The opt-in
+ * for the E4M3 / bf16 strategies, which the reference's QParams cannot express. */
+int groupgemm_mxmoe_fmt(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr_scale_b, void** ptr_Cs,
+                        void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
+                        mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
+                        mxmoe_qparams* h_qbits_list, int problem_count, const int32_t* h_fmts);
 
 /* Free groupgemm_mxmoe's per-device workspaces and staging buffers (waits for each device to be
  * idle first). Safe to call at any time; the next shim call re-allocates. */

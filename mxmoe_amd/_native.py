@@ -44,7 +44,7 @@ class MxmoeQParams(ctypes.Structure):
     """Layout of the reference's mxmoe::QParams (quantize.cuh:14-25): int2 qbits; int gsize; bool sym."""
 
     _fields_ = [("a_bits", ctypes.c_int32), ("w_bits", ctypes.c_int32), ("gsize", ctypes.c_int32),
-                ("sym", ctypes.c_uint8), ("fmt", ctypes.c_uint8), ("pad_", ctypes.c_uint8 * 2)]
+                ("sym", ctypes.c_uint8), ("pad_", ctypes.c_uint8 * 3)]
 
 
 class MxmoeDim3(ctypes.Structure):
@@ -70,6 +70,7 @@ class GGPlanInfo(ctypes.Structure):
         ("variant", ctypes.c_int32), ("problem_count", ctypes.c_int32), ("total_tiles", ctypes.c_int32),
         ("grid", ctypes.c_int32), ("block", ctypes.c_int32), ("lds_bytes", ctypes.c_int32),
         ("qtype_mask", ctypes.c_int32), ("splitk_slabs", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64), ("workspace", ctypes.c_void_p),
+        ("signature", ctypes.c_uint64),
     ]
 
 
@@ -77,8 +78,8 @@ class GGPlanInfo(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
-    "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_launch", "mxmoe_gg_run",
-    "groupgemm_mxmoe", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
+    "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_rebind", "mxmoe_gg_launch", "mxmoe_gg_run",
+    "groupgemm_mxmoe", "groupgemm_mxmoe_fmt", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     "mxmoe_gg_plan_tiles",
     # include/mxmoe_moe.h (MoE-layer plumbing)
     "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_combine",
@@ -115,6 +116,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_plan.restype = c.c_int
     lib.mxmoe_gg_plan.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.c_void_p, c.c_size_t, c.c_void_p,
                                   c.POINTER(GGPlanInfo)]
+    lib.mxmoe_gg_rebind.restype = c.c_int
+    lib.mxmoe_gg_rebind.argtypes = [c.POINTER(GGProblemC), c.c_int, c.POINTER(GGPlanInfo), c.c_void_p]
     lib.mxmoe_gg_launch.restype = c.c_int
     lib.mxmoe_gg_launch.argtypes = [c.POINTER(GGPlanInfo), c.c_void_p]
     lib.mxmoe_gg_run.restype = c.c_int
@@ -122,6 +125,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.groupgemm_mxmoe.restype = c.c_int
     lib.groupgemm_mxmoe.argtypes = [c.c_void_p] * 10 + [c.c_void_p, c.POINTER(MxmoeDim3), c.c_void_p,
                                                          c.POINTER(MxmoeQParams), c.c_int]
+    lib.groupgemm_mxmoe_fmt.restype = c.c_int
+    lib.groupgemm_mxmoe_fmt.argtypes = lib.groupgemm_mxmoe.argtypes + [c.c_void_p]
     lib.mxmoe_gg_release_shim_workspaces.restype = c.c_int
     lib.mxmoe_gg_release_shim_workspaces.argtypes = []
     lib.mxmoe_gg_repack_weightonly.restype = c.c_int

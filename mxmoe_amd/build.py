@@ -10,6 +10,9 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "lib" / "libmxmoe_gg.so"
+# tools-only lab library: the v2 family with the timing ablations and mainloop experiments
+# (-DMXMOE_LAB; tools/kbench.py with MXMOE_GG_LIB=<this>). Never loaded by the product.
+LAB_LIB = PKG / "lib" / "libmxmoe_gg_lab.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MXMOE_OFFLOAD_ARCH", "gfx950")
 
@@ -20,25 +23,27 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wa
          "-I", str(ROOT / "include")]
 
 
-def needs_build() -> bool:
-    if not LIB.exists():
+def needs_build(lib: Path = LIB) -> bool:
+    if not lib.exists():
         return True
-    t = LIB.stat().st_mtime
+    t = lib.stat().st_mtime
     return any(p.stat().st_mtime > t for p in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None) -> Path:
-    if not force and not needs_build():
-        return LIB
-    LIB.parent.mkdir(parents=True, exist_ok=True)
-    tmp = LIB.with_suffix(".so.tmp")
-    cmd = [HIPCC, *FLAGS, *(extra or []), "-o", str(tmp), *map(str, SOURCES)]
+def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None, lab: bool = False) -> Path:
+    out = LAB_LIB if lab else LIB
+    if not force and not needs_build(out):
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_suffix(".so.tmp")
+    defs = ["-DMXMOE_LAB"] if lab else []
+    cmd = [HIPCC, *FLAGS, *defs, *(extra or []), "-o", str(tmp), *map(str, SOURCES)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, lab="--lab" in sys.argv))

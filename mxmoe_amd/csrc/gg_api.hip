@@ -47,6 +47,18 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+// Planner A/B switches (MXMOE_GG_BAND, _REGION, _REGION_ROT, _ALIGN, _TAIL_CHUNK, _XCD_RR) are
+// read only by the tools-only lab build (-DMXMOE_LAB, libmxmoe_gg_lab.so): the product library's
+// tile placement never depends on the caller's environment.
+const char* planner_knob(const char* name) {
+#ifdef MXMOE_LAB
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 struct TileGeom {
   int bm, bn, bkb, threads;
 };
@@ -82,6 +94,20 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   } else if constexpr ((ABL & kWoAblMask) != 0) {
     launch_v2_q<ABL, 8>(a, grid, s);  // weight-only ablations: w4a16 tiles only
   } else {
+#ifdef MXMOE_LAB
+    // lab build: fp16, w8a8, w4a4, w8a8 + w4a4 (LP-1 mixed), w4a16, bf16 only (fast builds)
+    switch (qmask & 511) {
+      case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
+      case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
+      case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
+      case 6: launch_v2_q<ABL, 6>(a, grid, s); break;
+      case 8: launch_v2_q<ABL, 8>(a, grid, s); break;
+      case 256: launch_v2_q<ABL, 256>(a, grid, s); break;
+      default:
+        fprintf(stderr, "libmxmoe_gg_lab: quant-type mix %#x not compiled in the lab build\n", qmask);
+        abort();
+    }
+#else
     switch (qmask & 511) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
       case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
@@ -89,6 +115,7 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       case 6: launch_v2_q<ABL, 6>(a, grid, s); break;
       case 7: launch_v2_q<ABL, 7>(a, grid, s); break;
       case 8: launch_v2_q<ABL, 8>(a, grid, s); break;    // w4a16 only
+      case 10: launch_v2_q<ABL, 10>(a, grid, s); break;  // w4a16 + w8a8 (the reference's hz_fused pairing)
       case 16: launch_v2_q<ABL, 16>(a, grid, s); break;  // w8a16 only
       case 32: launch_v2_q<ABL, 32>(a, grid, s); break;  // w4a4 g128 only
       case 64: launch_v2_q<ABL, 64>(a, grid, s); break;  // w2a16 only
@@ -104,6 +131,7 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
         else launch_v2_q<0, 63>(a, grid, s);
         break;
     }
+#endif
   }
 }
 
@@ -183,34 +211,47 @@ typedef TileCfg<128, 128, 2, 2, 2> T128x128;
 typedef TileCfg<256, 128, 2, 2, 1> T256x128;
 typedef TileCfg<128, 256, 2, 2, 1> T128x256;
 
+// Production variants (libmxmoe_gg.so): every one computes correct results. The lab build
+// (-DMXMOE_LAB -> libmxmoe_gg_lab.so, tools only: `python -m mxmoe_amd.build --lab`) compiles the
+// v2 family only, with the timing ablations (abl_*, WRONG RESULTS by design) and the mainloop
+// experiments, for tools/kbench.py A/B runs (MXMOE_GG_LIB=mxmoe_amd/lib/libmxmoe_gg_lab.so).
 const std::vector<Variant>& variants() {
   static const std::vector<Variant> v = {
+#ifndef MXMOE_LAB
       make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
       make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
       make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
       make_v2("v2_256x256_w8_dma"),
       make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
-      // timing ablations of v2 (WRONG RESULTS by design; tools/kbench.py A/B only)
-      make_v2<ABL_NO_DMA>("abl_v2_nodma"),
-      make_v2<ABL_NO_EPI>("abl_v2_noepi"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
+      // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB): AUTO for short-K calls
+      make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
+#else
+      make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
+      make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
+      // mainloop experiments (correct results)
+      make_v2<V2_STAGGER | (1 << V2_SPREAD_SHIFT)>("x_v2s_spread1"),
+      make_v2<V2_STAGGER | (2 << V2_SPREAD_SHIFT)>("x_v2s_spread2"),
+      make_v2<V2_STAGGER | (4 << V2_SPREAD_SHIFT)>("x_v2s_spread4"),
+      make_v2<V2_STAGGER | V2_BUF>("x_v2s_buf"),
+      make_v2<V2_STAGGER | V2_BUF | (2 << V2_SPREAD_SHIFT)>("x_v2s_buf_spread2"),
+      make_v2<V2_STAGGER | V2_BUF | (4 << V2_SPREAD_SHIFT)>("x_v2s_buf_spread4"),
       // timing ablations of the staggered v2 (WRONG RESULTS by design; int8 tiles only)
       make_v2<V2_STAGGER | ABL_NO_DMA>("abl_v2s_nodma"),
       make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
       make_v2<V2_STAGGER | ABL_NO_DMA | ABL_NO_EPI>("abl_v2s_nodma_noepi"),
       make_v2<V2_STAGGER | V2_TRACE>("abl_v2s_trace"),
       make_v2<V2_STAGGER | ABL_DMA_HOT>("abl_v2s_dmahot"),
-      // where the DMA cost goes (v2, WRONG RESULTS by design; int8 tiles only)
+      // where the DMA cost goes (plain v2; int8 tiles only)
       make_v2<ABL_B_NODMA>("abl_v2_b_nodma"),
       make_v2<ABL_B_REGLOAD>("abl_v2_b_regload"),
       make_v2<ABL_B_TILED>("abl_v2_b_tiled"),
-      // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB): AUTO for short-K calls
-      make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
-      // weight-only timing ablations (WRONG RESULTS by design; w4a16 tiles only)
+      // weight-only timing ablations (w4a16 tiles only)
       make_v2<V2_STAGGER | ABL_WO_BTILED>("abl_v2s_wo_btiled"),
       make_v2<V2_STAGGER | ABL_WO_NODMA>("abl_v2s_wo_nodma"),
       make_v2<V2_STAGGER | ABL_WO_NOCOMPUTE>("abl_v2s_wo_nocompute"),
+#endif
   };
   return v;
 }
@@ -372,6 +413,9 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   const int64_t ldc = p.ldc ? p.ldc : p.N;
   if (lda_b < kbytes || ldb_b < kbytes || (lda_b % 16) || (ldb_b % 16))
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: lda/ldb must be >= K row and a multiple of 8 words", idx);
+  // the buffer-form LDS-DMA addresses a 256-row tile with 32-bit offsets below 2^31
+  if (lda_b >= (int64_t)1 << 23 || ldb_b >= (int64_t)1 << 23)
+    return fail(MXMOE_GG_ERR_INVALID, "problem %d: A / B row strides must be below 8 MiB", idx);
   if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
   if (check_ptrs && p.M > 0 && p.N > 0) {  // empty problems are dropped by the planner
     if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
@@ -506,7 +550,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return tile_cost[a] > tile_cost[b]; });
 
   // m-tiles per band (n-major inside a band): a 32-tile chunk is band x (32 / band) tiles
-  const char* band_env = getenv("MXMOE_GG_BAND");  // A/B switch (default 4)
+  const char* band_env = planner_knob("MXMOE_GG_BAND");  // A/B switch (default 4)
   const size_t band = band_env && atoi(band_env) > 0 ? (size_t)atoi(band_env) : 4;
   plan->meta.clear();
   plan->order = order;
@@ -521,12 +565,12 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // transpose) — the split of the grid into 8 rectangles is chosen to minimise that sum.
   // placement: after the chunked tiles (default; measured 1-5 % faster than at the queue head on the
   // w8a8 gate_up / down / mixed calls, profiles/r02/region/)
-  const char* region_env = getenv("MXMOE_GG_REGION");  // A/B switch: 0 off, 1 queue head, 2 tail (default)
+  const char* region_env = planner_knob("MXMOE_GG_REGION");  // A/B switch: 0 off, 1 queue head, 2 tail (default)
   const bool regions_on = !(region_env && region_env[0] == '0');
   const bool regions_last = !(region_env && region_env[0] == '1');
-  const char* rot_env = getenv("MXMOE_GG_REGION_ROT");  // A/B switch (default off)
+  const char* rot_env = planner_knob("MXMOE_GG_REGION_ROT");  // A/B switch (default off)
   const bool region_rot = rot_env && rot_env[0] == '1';
-  const char* align_env = getenv("MXMOE_GG_ALIGN");  // A/B switch: problem-aligned chunks (default on)
+  const char* align_env = planner_knob("MXMOE_GG_ALIGN");  // A/B switch: problem-aligned chunks (default on)
   const bool align_on = !(align_env && align_env[0] == '0');
   struct Region {
     int gm = 0, gn = 0, r = 0, c = 0;
@@ -651,9 +695,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   };
   if (!regions_last) put_regions();
   const int TS = (int)seq.size();
-  const char* tc_env = getenv("MXMOE_GG_TAIL_CHUNK");  // A/B switch: tail chunk size (default 16)
+  const char* tc_env = planner_knob("MXMOE_GG_TAIL_CHUNK");  // A/B switch: tail chunk size (default 16)
   const int tail_chunk = tc_env && atoi(tc_env) > 0 ? atoi(tc_env) : 16;
-  const char* rr_env = getenv("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
+  const char* rr_env = planner_knob("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
   const bool round_robin = rr_env && rr_env[0] == '1';
   for (int s0 = 0, c = 0; s0 < TS; ++c) {
     const bool head = TS - s0 > 16 * chunk;
@@ -783,6 +827,20 @@ std::vector<uint8_t> workspace_image(const Plan& plan, const std::vector<const v
   return img;
 }
 
+// FNV-1a over the plan table and the tile table: equal for two calls with the same shapes, quant
+// params and strides (the planner is deterministic), whatever their buffers.
+uint64_t plan_signature(const Plan& plan) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  mix(plan.meta.data(), plan.meta.size() * sizeof(GGMeta));
+  mix(plan.tiles.data(), plan.tiles.size() * sizeof(TileDesc));
+  mix(plan.order.data(), plan.order.size() * sizeof(int));
+  return h;
+}
+
 void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe_gg_plan_info* info) {
   const Variant& v = variants()[variant];
   info->variant = variant;
@@ -796,6 +854,7 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
   info->splitk_slabs = plan.slabs;
   info->workspace_bytes = (int64_t)l.total;
   info->workspace = ws;
+  info->signature = plan_signature(plan);
 }
 
 }  // namespace
@@ -932,6 +991,33 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
   return MXMOE_GG_OK;
 }
 
+int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const mxmoe_gg_plan_info* info,
+                    void* stream) {
+  if (problem_count < 0 || (problem_count > 0 && !problems) || !info || !info->workspace)
+    return fail(MXMOE_GG_ERR_INVALID, "bad arguments to mxmoe_gg_rebind");
+  int st = check_variant(info->variant);
+  if (st) return st;
+  const std::vector<HostProblem> hp = to_host(problems, problem_count);
+  Plan plan;
+  st = plan_host(hp, info->variant, true, &plan);
+  if (st) return st;
+  if (plan_signature(plan) != info->signature || (int)plan.meta.size() != info->problem_count)
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_gg_rebind: problems differ from the planned call (shapes, quant "
+                                      "params or strides); plan again");
+  const WsLayout l = ws_layout(info->problem_count, info->grid, info->splitk_slabs);
+  std::vector<uint8_t> cols(5 * l.ptr, 0);
+  for (int c = 0; c < 5; ++c)
+    for (size_t i = 0; i < plan.order.size(); ++i) {
+      const HostProblem& q = hp[plan.order[i]];
+      const void* p = c == 0 ? q.A : c == 1 ? q.B : c == 2 ? q.SA : c == 3 ? q.SB : q.C;
+      memcpy(cols.data() + c * l.ptr + i * sizeof(void*), &p, sizeof(void*));
+    }
+  HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(info->workspace) + l.meta, cols.data(), cols.size(),
+                         hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // pageable host columns must outlive the copy
+  return MXMOE_GG_OK;
+}
+
 int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   if (!info) return fail(MXMOE_GG_ERR_INVALID, "NULL plan");
   int st = check_variant(info->variant);
@@ -1033,6 +1119,14 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
                     void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
                     mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
                     mxmoe_qparams* h_qbits_list, int problem_count) {
+  return groupgemm_mxmoe_fmt(ptr_As, ptr_Bs, ptr_scale_a, ptr_scale_b, ptr_Cs, ptr_Ds, ldas, ldbs, ldcs, ldds,
+                             problem_sizes, h_problem_sizes, qbits_list, h_qbits_list, problem_count, nullptr);
+}
+
+int groupgemm_mxmoe_fmt(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr_scale_b, void** ptr_Cs,
+                        void** ptr_Ds, int64_t* ldas, int64_t* ldbs, int64_t* ldcs, int64_t* ldds,
+                        mxmoe_dim3* problem_sizes, mxmoe_dim3* h_problem_sizes, mxmoe_qparams* qbits_list,
+                        mxmoe_qparams* h_qbits_list, int problem_count, const int32_t* h_fmts) {
   (void)ptr_Ds;
   (void)ldas;
   (void)ldbs;
@@ -1066,7 +1160,7 @@ int groupgemm_mxmoe(void** ptr_As, void** ptr_Bs, void** ptr_scale_a, void** ptr
                         h[3 * problem_count + i], h[4 * problem_count + i], (int)h_problem_sizes[i].x,
                         (int)h_problem_sizes[i].y, (int)h_problem_sizes[i].z, h_qbits_list[i].a_bits,
                         h_qbits_list[i].w_bits, h_qbits_list[i].gsize, h_qbits_list[i].sym, 0, 0, 0,
-                        h_qbits_list[i].fmt};
+                        h_fmts ? (int)h_fmts[i] : (int)MXMOE_GG_FMT_DEFAULT};  // never QParams' padding
   // 2. same shapes as the last call on this device: reuse its plan (the pointers still get the same
   //    NULL / alignment checks as mxmoe_gg_plan)
   std::vector<int64_t> key;

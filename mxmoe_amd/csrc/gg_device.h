@@ -562,6 +562,15 @@ enum : int {
   ABL_B_REGLOAD = 1024,  // ablation: B operand loaded into registers (same global traffic), not into LDS
   ABL_B_TILED = 2048,    // ablation: B read as if stored in contiguous 32-KiB (256 rows x 128 B) stage blocks
   V2_B3 = 4096,          // stagger: B in a 3-stage LDS ring, two stages ahead (A: 2 stages, one ahead)
+  // spread (bits 18-20 = k): the stage's LDS-DMA pieces are issued one per k MFMAs inside the first
+  // MFMA half of the stagger loop (sched_group_barrier) instead of as a burst at its top
+  V2_SPREAD_SHIFT = 18,
+  // buffer-form LDS-DMA: `buffer_load_dwordx4 ... lds` from a per-tile buffer resource (A / B base
+  // row m0 / n0 in SGPRs), a 32-bit lane offset fixed for the whole tile and the stage's K offset in
+  // soffset: no per-piece address VALU, 1 VGPR per piece instead of 2; K-tail chunks are offset
+  // past num_records (the hardware returns zeros). Rows of a tile must span < 2 GiB (the planner
+  // checks the row strides).
+  V2_BUF = 1 << 21,
   // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
   // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
   ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
@@ -605,6 +614,7 @@ struct V2Half {
   typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
   static constexpr int FM = Cfg::FM, FN = Cfg::FN;
   static constexpr int SUBH = (QT == QT_I4) ? 2 : 1;  // MFMA K steps per 64-B half stage
+  static constexpr int kMfma = SUBH * FM * FN, kReads = SUBH * (FM + FN);  // per half stage
   word_t a[SUBH][FM];
   word_t b[SUBH][FN];
 
@@ -696,6 +706,28 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         srcB[j] = B + (int64_t)(n0 / 256) * ((kbytes + 127) / 128) * 32768 + row * 128 + ((p ^ ((row >> 1) & 7)) << 4);
     }
   }
+  // V2_BUF: per-tile buffer resources and fixed 32-bit lane offsets (rows relative to m0 / n0)
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(A) + (int64_t)m0 * lda, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B) + (int64_t)n0 * ldb, (short)0, 0x7fffffff, 0x00020000);
+  uint32_t voA[GA], voB[GB];
+  {
+    const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int row = (wave * GA + j) * 8 + rsub;
+      voA[j] = (uint32_t)((min(m0 + row, M - 1) - m0) * lda) + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = (wave * GB + j) * 8 + rsub;
+      voB[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb) + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+  }
+  auto bdma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t vo, int kb, uint8_t* dst) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, vo, kb, 0, 0);
+  };
   uint4 breg[GB];  // ABL_B_REGLOAD sink
   auto issue = [&](int s, int buf) {
     if constexpr ((ABL & ABL_NO_DMA) != 0) {
@@ -704,6 +736,21 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     uint8_t* As = lds + buf * Cfg::STAGE_BYTES;
     uint8_t* Bs = As + Cfg::A_BYTES;
     const int kb = (ABL & ABL_DMA_HOT) ? ks0 * Cfg::BKB : (ks0 + s) * Cfg::BKB;
+    if constexpr ((ABL & V2_BUF) != 0) {
+      const bool full = kb + Cfg::BKB <= kbytes;
+      const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const int kc = (p ^ ((((wave * GA + j) * 8 + rsub) >> 1) & 7)) << 4;
+        bdma(rsA, full || kb + kc < kbytes ? voA[j] : 0x80000000u, kb, As + (wave * GA + j) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int kc = (p ^ ((((wave * GB + j) * 8 + rsub) >> 1) & 7)) << 4;
+        bdma(rsB, full || kb + kc < kbytes ? voB[j] : 0x80000000u, kb, Bs + (wave * GB + j) * 1024);
+      }
+      return;
+    }
     if (kb + Cfg::BKB <= kbytes) {
 #pragma unroll
       for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
@@ -897,6 +944,108 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
     stash_scale();  // the rings are dead: the scale stash (past the epilogue image) is free
     if constexpr (qt_scaled(QT)) __syncthreads();
+  } else if constexpr ((ABL & V2_STAGGER) != 0 && ((ABL >> V2_SPREAD_SHIFT) & 7) != 0) {
+    // staggered v2 with the stage's LDS-DMA spread over the MFMAs: the steady-state iterations
+    // (stage s+1 a full 128-B stage) are one basic block each, ordered by sched_group_barrier as
+    //   early waves: ds_read half 0 | {k MFMA, 1 DMA piece} x (GA+GB) | rest of half 0 | ds_read half 1 | MFMA half 1
+    //   late waves:  {1 DMA piece, k MFMA} x (GA+GB) | rest of the deferred half | ds_read | MFMA | ds_read
+    // then vmcnt(0) + barrier as v2s. The K-tail stage and the late waves' first stage run the v2s body.
+    typedef V2Half<Cfg, QT> Half;
+    constexpr int NH = Half::kMfma, NR = Half::kReads, ND = GA + GB;
+    constexpr int KS0 = (ABL >> V2_SPREAD_SHIFT) & 7, KS = KS0 * ND <= NH ? KS0 : NH / ND;  // small tiles: denser
+    static_assert(KS >= 1, "spread: more DMA pieces than MFMAs in a half stage");
+    auto hread = [&](Half& f, int buf, int h) {
+      f.read(lds + buf * Cfg::STAGE_BYTES, lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES, a_row, b_row, swz, g, h);
+    };
+    auto hmma = [&](const Half& f) { f.mma(acc); };
+    auto dma_full = [&](int t) {  // stage t (a full 128-B stage) into buffer t & 1
+      uint8_t* As = lds + (t & 1) * Cfg::STAGE_BYTES;
+      uint8_t* Bs = As + Cfg::A_BYTES;
+      const int kb = (ks0 + t) * Cfg::BKB;
+      if constexpr ((ABL & V2_BUF) != 0) {
+#pragma unroll
+        for (int j = 0; j < GA; ++j) bdma(rsA, voA[j], kb, As + (wave * GA + j) * 1024);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) bdma(rsB, voB[j], kb, Bs + (wave * GB + j) * 1024);
+      } else {
+#pragma unroll
+        for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
+      }
+    };
+    auto sync = [&]() {
+      wait_vmcnt<0>();
+      lds_barrier();
+    };
+    const int nfull = nst - 1 - ((ks0 + nst) * Cfg::BKB > kbytes ? 1 : 0);  // iterations issuing a full stage
+    if (nst > 0) {
+      Half fr;
+      issue(0, 0);
+      __syncthreads();
+      stash_scale();
+      if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
+        if (nst > 1) issue(1, 1);
+        hread(fr, 0, 0);
+        hmma(fr);
+        hread(fr, 0, 1);
+        sync();
+        int s = 1;
+        for (; s < nfull; ++s) {
+          dma_full(s + 1);
+          hmma(fr);  // second half of stage s-1
+          hread(fr, s & 1, 0);
+          hmma(fr);
+          hread(fr, s & 1, 1);
+#pragma unroll
+          for (int q = 0; q < ND; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          sync();
+        }
+        for (; s < nst; ++s) {
+          if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
+          hmma(fr);
+          hread(fr, s & 1, 0);
+          hmma(fr);
+          hread(fr, s & 1, 1);
+          sync();
+        }
+        hmma(fr);
+      } else {  // early waves
+        int s = 0;
+        for (; s < nfull; ++s) {
+          hread(fr, s & 1, 0);
+          dma_full(s + 1);
+          hmma(fr);
+          hread(fr, s & 1, 1);
+          hmma(fr);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+          for (int q = 0; q < ND; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          sync();
+        }
+        for (; s < nst; ++s) {
+          if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
+          hread(fr, s & 1, 0);
+          hmma(fr);
+          hread(fr, s & 1, 1);
+          hmma(fr);
+          sync();
+        }
+      }
+    }
   } else if constexpr ((ABL & V2_STAGGER) != 0) {
     typedef V2Half<Cfg, QT> Half;
     auto hread = [&](Half& f, int buf, int h) {

@@ -300,6 +300,34 @@ def ep_layer_chunks(plan: list[list[RowItem]], gate_up: Sequence[QShape], down: 
     return out
 
 
+XGMI_LINK_GBS = 64.0  # effective all-gather GB/s per xGMI link and direction (of ~153 GB/s raw per link)
+CHUNK_OVERHEAD_MS = 0.015  # per extra chunk: two more launches + one more ragged finish per call
+
+
+def gather_ms_model(bytes_received: float, world: int) -> float:
+    """Modelled all-gather time: on a fully connected node every rank receives each peer's shard over
+    its own xGMI link, so (world - 1) links carry the bytes in parallel."""
+    if world <= 1:
+        return 0.0
+    return bytes_received / ((world - 1) * XGMI_LINK_GBS * 1e9) * 1e3
+
+
+def choose_chunks(t_compute_ms: float, t_gather_ms: float, max_chunks: int = 8,
+                  overhead_ms: float = CHUNK_OVERHEAD_MS) -> int:
+    """Chunk count of EPLayerStep's compute / all-gather pipeline. With c chunks, chunk i's gather
+    runs beside chunk i+1's compute, so the step takes about
+        max(Tc, Tg) + min(Tc, Tg) / c + (c - 1) * overhead
+    (the longer stream, plus the first compute or last gather chunk that nothing hides, plus the
+    cost of cutting the calls finer); returns the c in [1, max_chunks] that minimises it."""
+    lo, hi = sorted((max(t_compute_ms, 0.0), max(t_gather_ms, 0.0)))
+    best, best_t = 1, None
+    for c in range(1, max_chunks + 1):
+        t = hi + lo / c + (c - 1) * overhead_ms
+        if best_t is None or t < best_t - 1e-12:
+            best, best_t = c, t
+    return best
+
+
 class EPLayerStep:
     """This rank's part of one layer split by ``ep_layer_plan``: per chunk (``ep_layer_chunks``) one
     planned gate_up call and one down call over its row items, and one all_gather_into_tensor of

@@ -126,6 +126,25 @@ class Problem:
     ldb: int = 0
     ldc: int = 0
 
+    def __post_init__(self):
+        """Operand dtypes must match q's format: the C-ABI sees only bytes, so an fp16 operand
+        labelled bf16 (or float data labelled as integer codes) would run and return garbage."""
+        def need(t, ok, what):
+            if t is not None and t.numel() > 0 and t.dtype not in ok:  # (empty: a planning placeholder)
+                raise ValueError(f"{self.q.qcfg}: {what} must be {' / '.join(map(str, ok))}, got {t.dtype}")
+
+        codes = (torch.uint8, torch.int8, torch.int16, torch.uint16, torch.int32, torch.float8_e4m3fn)
+        if self.q.fmt == "bf16":
+            need(self.A, (torch.bfloat16,), "A")
+            need(self.B, (torch.bfloat16,), "B")
+        elif not self.q.is_quant:
+            need(self.A, (torch.float16,), "A")
+            need(self.B, (torch.float16,), "B")
+        else:
+            need(self.A, (torch.float16,) if self.q.is_weight_only else codes, "A")
+            need(self.B, codes, "B (packed codes)")
+        need(self.C, (torch.float16,), "C")
+
     def to_c(self) -> nat.GGProblemC:
         def ptr(t):
             return 0 if t is None else t.data_ptr()
@@ -187,6 +206,19 @@ class GroupGemm:
     def flops(self) -> int:
         return sum(p.flops for p in self.problems)
 
+    def rebind(self, problems: Sequence[Problem], stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Point the plan at new operand buffers of the same shapes / quant params / strides
+        (mxmoe_gg_rebind: uploads the pointer columns only; GGError if the shapes differ)."""
+        problems = list(problems)
+        for p in problems:
+            for t in (p.A, p.B, p.C, p.scale_a, p.scale_b):
+                if t is not None and t.device != self.device:
+                    raise ValueError(f"all tensors must live on {self.device}, got {t.device}")
+        P = len(problems)
+        cps = (nat.GGProblemC * max(P, 1))(*[p.to_c() for p in problems])
+        nat.check(nat.lib().mxmoe_gg_rebind(cps, P, ctypes.byref(self.info), ctypes.c_void_p(_stream_handle(stream))))
+        self.problems, self._c_problems = problems, cps
+
     def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         nat.check(nat.lib().mxmoe_gg_launch(ctypes.byref(self.info), ctypes.c_void_p(_stream_handle(stream))))
 
@@ -201,17 +233,24 @@ def group_gemm(problems: Sequence[Problem], variant: Optional[int] = None,
 
 def groupgemm_reference_abi(ptr_As: torch.Tensor, ptr_Bs: torch.Tensor, ptr_scale_a: torch.Tensor,
                             ptr_scale_b: torch.Tensor, ptr_Cs: torch.Tensor, h_problem_sizes: Sequence[tuple],
-                            h_qbits_list: Sequence[QParams]) -> None:
+                            h_qbits_list: Sequence[QParams], pad_byte: int = 0) -> None:
     """Call the drop-in ``groupgemm_mxmoe`` entry (reference FuncType, registry.cuh:28-39).
 
     ``ptr_*`` are int64 device tensors holding device pointers (the reference's device arrays).
+    ``pad_byte`` fills the three padding bytes of every QParams (the reference leaves them
+    uninitialised; the library must ignore them). Problems with a non-default operand format (E4M3,
+    bf16 — not expressible in the reference's QParams) go through ``groupgemm_mxmoe_fmt``.
     """
     P = len(h_problem_sizes)
     dims = (nat.MxmoeDim3 * max(P, 1))(*[nat.MxmoeDim3(int(m), int(n), int(k)) for (m, n, k) in h_problem_sizes])
     qps = (nat.MxmoeQParams * max(P, 1))(
-        *[nat.MxmoeQParams(q.a_bits, q.w_bits, q.gsize, int(q.sym), q.fmt_code, (ctypes.c_uint8 * 2)())
+        *[nat.MxmoeQParams(q.a_bits, q.w_bits, q.gsize, int(q.sym), (ctypes.c_uint8 * 3)(pad_byte, pad_byte, pad_byte))
           for q in h_qbits_list])
     dev_dims = torch.tensor([[m, n, k] for (m, n, k) in h_problem_sizes], dtype=torch.int32, device=ptr_As.device)
-    nat.check(nat.lib().groupgemm_mxmoe(
-        ptr_As.data_ptr(), ptr_Bs.data_ptr(), ptr_scale_a.data_ptr(), ptr_scale_b.data_ptr(), ptr_Cs.data_ptr(),
-        None, None, None, None, None, ctypes.c_void_p(dev_dims.data_ptr()), dims, None, qps, P))
+    args = (ptr_As.data_ptr(), ptr_Bs.data_ptr(), ptr_scale_a.data_ptr(), ptr_scale_b.data_ptr(), ptr_Cs.data_ptr(),
+            None, None, None, None, None, ctypes.c_void_p(dev_dims.data_ptr()), dims, None, qps, P)
+    if any(q.fmt_code != nat.FMT_DEFAULT for q in h_qbits_list):
+        fmts = (ctypes.c_int32 * max(P, 1))(*[q.fmt_code for q in h_qbits_list])
+        nat.check(nat.lib().groupgemm_mxmoe_fmt(*args, fmts))
+    else:
+        nat.check(nat.lib().groupgemm_mxmoe(*args))

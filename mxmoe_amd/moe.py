@@ -283,6 +283,71 @@ def silu_mul_then_quant(inp: torch.Tensor, num_problems: int, num_experts: int, 
     return inp_list, scale_list, out_list, b.out, b.scales, out_store
 
 
+_SHARE_FUSED_PLANS: dict = {}
+
+
+def gg_mxmoe_share_fused(inp: Sequence[torch.Tensor], experts: Sequence[torch.Tensor],
+                         scale_zp_a: Sequence[torch.Tensor], scale_zp_b: Sequence[torch.Tensor],
+                         output: Sequence[torch.Tensor], N: int, K: int, shared_N: int, shared_K: int,
+                         qparams_per_exp, recv_tokens_per_exp: torch.Tensor, verbose: bool = False,
+                         stream: Optional[torch.cuda.Stream] = None):
+    """Mirror of the reference's fused GroupGEMM op (ref_bind.cu:312-431, pybind name
+    ``gg_mxmoe_share_fused``), with its argument meaning:
+
+    * ``recv_tokens_per_exp`` int64 [E] (host or device): routed rows per expert; experts with 0
+      rows have no problem. ``experts`` has E entries, or E + 1 with the shared expert last, whose
+      problem has ``inp[-1].size(0)`` rows and shape (shared_N, shared_K); routed ones (N, K).
+    * ``inp`` / ``scale_zp_a`` / ``output`` are per PROBLEM (non-empty experts in expert order, then
+      the shared one), ``experts`` / ``scale_zp_b`` / ``qparams_per_exp`` per EXPERT;
+      qparams_per_exp[e] = (a_bits, w_bits, gsize, sym).
+    * Operands are in the GroupGEMM layout (the outputs of ``quant_inp_act`` /
+      ``silu_mul_then_quant`` and ``prepare_weight``); an empty scale tensor means "no scale" (fp16).
+
+    The reference hard-codes one fused w4a16 + w8a8 kernel (``mxmoe_w4a16_w8a8_bs256``, :412); here
+    any supported mix runs on the AUTO variant. The plan (tile table) is cached per shape / qparams
+    signature, so repeated calls with the same routing only re-point the operands. Returns ``output``.
+    """
+    counts = [int(c) for c in recv_tokens_per_exp.tolist()]
+    E = len(counts)
+    has_shared = len(experts) > E
+    num_tokens = int(inp[-1].shape[0]) if len(inp) else 0
+    probs = []
+    pi = 0
+    for e in range(E + (1 if has_shared else 0)):
+        rows = num_tokens if e == E else counts[e]
+        if rows == 0:
+            continue
+        if pi >= len(inp):
+            raise ValueError(f"gg_mxmoe_share_fused: {len(inp)} inputs for more non-empty experts")
+        a_bits, w_bits, gsize, sym = (int(x) for x in qparams_per_exp[e])
+        q = QParams(a_bits, w_bits, gsize, bool(sym))
+        n, k = (shared_N, shared_K) if e == E else (N, K)
+
+        def opt(t):
+            return None if t is None or t.numel() == 0 else t
+
+        C = output[pi]
+        probs.append(Problem(A=inp[pi], B=experts[e], C=C, M=rows, N=n, K=k, q=q, scale_a=opt(scale_zp_a[pi]),
+                             scale_b=opt(scale_zp_b[e]), ldc=int(C.stride(0)) if C.dim() == 2 else 0))
+        if verbose:
+            print(f"problem {pi}: [{rows},{n},{k}] qparams: [{a_bits} {w_bits}] {gsize} {int(bool(sym))}")
+        pi += 1
+    if pi != len(inp):
+        raise ValueError(f"gg_mxmoe_share_fused: {len(inp)} inputs for {pi} non-empty experts")
+    if not probs:
+        return output
+    key = (probs[0].C.device, tuple((p.M, p.N, p.K, p.q) for p in probs))
+    gg = _SHARE_FUSED_PLANS.get(key)
+    if gg is None:
+        if len(_SHARE_FUSED_PLANS) >= 64:
+            _SHARE_FUSED_PLANS.clear()
+        gg = _SHARE_FUSED_PLANS[key] = GroupGemm(probs, stream=stream)
+    else:
+        gg.rebind(probs, stream=stream)
+    gg.launch(stream)
+    return output
+
+
 # ------------------------------------------------------------------ the MoE FFN layer
 
 @dataclasses.dataclass

@@ -263,6 +263,38 @@ def ds2_mixed_qconfig(seed: int = 0, frac: float = 0.25, layer: int = 1) -> dict
     return {str(layer): {"experts": experts}}
 
 
+def w4a16_w8a8_qconfig(seed: int = 0, frac: float = 1.0 / 16, layer: int = 11) -> dict:
+    """qwen2_moe small-batch mixed scheme: w4a16_g-1_asym + w8a8_g-1_sym per linear block, the pairing
+    the reference hand-instantiates as one fused kernel (hz_fused.cuh:14-125, QConfig<half, false, 4,
+    -1, ...> + QCFG_W8A8; mxmoe_w4a16_w8a8_bs256 at ref_bind.cu:412). frac = 1/16 of the weight units
+    w8a8 gives the reference's published "W4.25A15.5" average (8/16 + 4 * 15/16 = 4.25 weight bits,
+    8/16 + 16 * 15/16 = 15.5 activation bits). Same seeded greedy scan as
+    ds2_mixed_qconfig; the shared expert (index E, 4x the intermediate width) weighs 4 units."""
+    E = MODEL_SHAPES["qwen2_moe"]["E"]
+    blocks = [(e, lin) for e in range(E + 1) for lin in ("gate_up", "down")]
+
+    def units(e: int, lin: str) -> int:
+        return (4 if e == E else 1) * (2 if lin == "gate_up" else 1)
+
+    budget = frac * sum(units(*b) for b in blocks)
+    w8, used = set(), 0
+    for i in np.random.default_rng(seed).permutation(len(blocks)):
+        b = blocks[int(i)]
+        if used + units(*b) <= budget:
+            w8.add(b)
+            used += units(*b)
+    w4a16 = {"w_bits": 4, "w_gsize": -1, "w_sym": False, "w_clip": [1.0, 1.0],
+             "a_bits": 16, "a_gsize": -1, "a_sym": True, "a_clip": [1.0, 1.0]}
+    w8a8 = {"w_bits": 8, "w_gsize": -1, "w_sym": True, "w_clip": [1.0, 1.0],
+            "a_bits": 8, "a_gsize": -1, "a_sym": True, "a_clip": [1.0, 1.0]}
+    experts = {}
+    for e in range(E + 1):
+        gu = w8a8 if (e, "gate_up") in w8 else w4a16
+        dn = w8a8 if (e, "down") in w8 else w4a16
+        experts[str(e)] = {"gate": dict(gu), "up": dict(gu), "down": dict(dn)}
+    return {str(layer): {"experts": experts}}
+
+
 def mixed_qconfig_lp1() -> dict:
     """The committed mixed w4a4+w8a8 (wbits 5.0) qconfig solved from the reference's bits_model-1.lp."""
     return load_qconfig(WORKLOAD_DIR / "qconfig_qwen2_moe_w4a4+w8a8_wbits5.0_lp1.json")

@@ -41,7 +41,7 @@ def test_struct_layouts():
 
 
 def test_abi_version_and_variants():
-    assert nat.lib().mxmoe_gg_abi_version() == 4
+    assert nat.lib().mxmoe_gg_abi_version() == 5
     vs = nat.list_variants()
     assert len(vs) == nat.variant_count() >= 1
     assert "w8a8_g-1_sym=TileConfig(" in vs[0]
@@ -61,7 +61,7 @@ def test_workspace_size_grows_with_tiles():
 
 
 def test_struct_plan_info_layout():
-    assert ctypes.sizeof(nat.GGPlanInfo) == 8 * 4 + 8 + 8  # qtype_mask + reserved keep the int64 aligned
+    assert ctypes.sizeof(nat.GGPlanInfo) == 8 * 4 + 8 + 8 + 8  # + the plan signature
 
 
 def test_auto_variant_follows_quant_mix():

@@ -277,3 +277,19 @@ def test_ep_layer_chunks_partition_each_rank(chunks):
             loads = [sum(w.rows * (gu[w.problem].N * gu[w.problem].K + dn[w.problem].N * dn[w.problem].K) for w in cp[r])
                      for cp in cps]
             assert max(loads) < 1.35 * sum(loads) / chunks
+
+
+def test_choose_chunks_model():
+    from mxmoe_amd.dist import choose_chunks, gather_ms_model
+
+    assert choose_chunks(0.5, 0.0) == 1  # nothing to hide
+    assert choose_chunks(0.0, 0.3) == 1
+    # compute and gather comparable: pipelining pays, more chunks while the overhead stays small
+    assert choose_chunks(0.19, 0.33) > 1
+    assert choose_chunks(0.19, 0.33, overhead_ms=1.0) == 1
+    assert choose_chunks(1.0, 1.0) >= choose_chunks(0.2, 0.2)
+    assert 1 <= choose_chunks(5.0, 5.0) <= 8
+    # qwen2_moe layer 11 at N = 8: 147 MB received per rank over 7 links
+    t = gather_ms_model(147e6, 8)
+    assert 0.2 < t < 0.5 and gather_ms_model(147e6, 1) == 0.0
+    assert gather_ms_model(84e6, 2) > gather_ms_model(147e6, 8)

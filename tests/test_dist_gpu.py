@@ -89,9 +89,14 @@ def _ep_worker(rank, world, port, cfg, q, chunks=1):
 
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        kw = {"fp16": {}, "mixed": dict(qconfig=mixed_qconfig_lp1()), "w4a4_g128": dict(qstr="w4a4_g128_sym"),
-              "w4a16": dict(qstr="w4a16_g128_asym")}[cfg]
-        layer = load_workload(qwen2_layer11_workload(1024, **kw))["layer-11"]
+        if cfg == "ds2_mixed":  # BASELINE configs[4]: DeepSeek-V2-Lite, 64 routed + 2 shared experts, mixed
+            from mxmoe_amd.workload import ds2_mixed_qconfig, ds2_workload
+
+            layer = load_workload(ds2_workload(1024, qconfig=ds2_mixed_qconfig()))["layer-1"]
+        else:
+            kw = {"fp16": {}, "mixed": dict(qconfig=mixed_qconfig_lp1()), "w4a4_g128": dict(qstr="w4a4_g128_sym"),
+                  "w4a16": dict(qstr="w4a16_g128_asym")}[cfg]
+            layer = load_workload(qwen2_layer11_workload(1024, **kw))["layer-11"]
         inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=7 + (gg == "down")) for gg in ("gate_up", "down")}
         step = EPLayerStep(inp["gate_up"], inp["down"], world, rank, chunks=chunks)
         s = torch.cuda.current_stream(dev)
@@ -123,7 +128,8 @@ def _ep_worker(rank, world, port, cfg, q, chunks=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,chunks", [("mixed", 1), ("fp16", 1), ("w4a4_g128", 1), ("w4a16", 1), ("mixed", 2)])
+@pytest.mark.parametrize("cfg,chunks", [("mixed", 1), ("fp16", 1), ("w4a4_g128", 1), ("w4a16", 1), ("mixed", 2),
+                                        ("ds2_mixed", 1), ("ds2_mixed", 3)])
 def test_ep_layer_step_matches_full_call(cfg, chunks):
     world = 2
     ctx = mp.get_context("spawn")

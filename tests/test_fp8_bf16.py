@@ -121,11 +121,11 @@ def test_workload_fmt_round_trip_keeps_reference_json():
     assert QShape(shape=[1, 8, 16], fmt="bf16").qcfg == "bf16"
 
 
-def test_abi_fmt_fields_sit_in_the_reference_padding():
-    assert nat.MxmoeQParams.sym.offset == 12 and nat.MxmoeQParams.fmt.offset == 13
+def test_abi_qparams_padding_and_fmt_field():
+    assert nat.MxmoeQParams.sym.offset == 12 and nat.MxmoeQParams.pad_.offset == 13
     assert ctypes.sizeof(nat.MxmoeQParams) == 16
     assert nat.GGProblemC.fmt.offset == nat.GGProblemC.sym.offset + 4
-    assert nat.lib().mxmoe_gg_abi_version() == 4
+    assert nat.lib().mxmoe_gg_abi_version() == 5
 
 
 def _plan_error(probs, variant):

@@ -227,7 +227,7 @@ def test_64bit_offsets_large_c(q):
     torch.cuda.empty_cache()
 
 
-def _shim_call(hps):
+def _shim_call(hps, pad_byte=0):
     def ptrs(get):
         return torch.tensor([get(h.problem) for h in hps], dtype=torch.int64, device=DEV)
 
@@ -235,7 +235,18 @@ def _shim_call(hps):
         ptrs(lambda p: p.A.data_ptr()), ptrs(lambda p: p.B.data_ptr()),
         ptrs(lambda p: 0 if p.scale_a is None else p.scale_a.data_ptr()),
         ptrs(lambda p: 0 if p.scale_b is None else p.scale_b.data_ptr()), ptrs(lambda p: p.C.data_ptr()),
-        [(h.M, h.N, h.K) for h in hps], [h.q for h in hps])
+        [(h.M, h.N, h.K) for h in hps], [h.q for h in hps], pad_byte=pad_byte)
+
+
+@pytest.mark.parametrize("pad_byte", [0x01, 0x02, 0xAB])
+def test_reference_abi_shim_ignores_qparams_padding(pad_byte):
+    """The reference's QParams constructors leave the 3 bytes after `sym` uninitialised
+    (quantize.cuh:19-20): whatever they hold, the shim computes the default-format result."""
+    specs = [(33, 128, 256, W8A8), (65, 256, 512, W4A4), (20, 128, 128, FP16)]
+    hps = [HostProblem(M, N, K, q, seed=141 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
+    _shim_call(hps, pad_byte=pad_byte)
+    torch.cuda.synchronize()
+    _check(hps)
 
 
 def test_reference_abi_shim_growing_problem_count_and_release():

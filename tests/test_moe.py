@@ -236,6 +236,38 @@ def test_moe_ffn_stagewise_parity(gpu):
     assert torch.isfinite(out.float()).all()
 
 
+@pytest.mark.gpu
+def test_gg_mxmoe_share_fused_mirror(gpu):
+    """The reference-named fused GroupGEMM op (ref_bind.cu:312-431) on quant_inp_act's outputs:
+    per-problem inputs / scales / outputs, per-expert weights / qparams, the shared expert last.
+    Bit-exact against the oracle for every integer problem; a second call with new activations on
+    the same routing reuses the cached plan (mxmoe_gg_rebind) and is exact again."""
+    T, topk, E, H, N = 90, 4, 6, 256, 256
+    g = torch.Generator().manual_seed(21)
+    qs = [W8A8, W4A4, W8A8, W4A4, W8A8, W4A4, W8A8]  # shared expert last
+    qparams = [(q.a_bits, q.w_bits, q.gsize, q.sym) for q in qs]
+    ws = [moe.prepare_weight((((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half()).to(DEV), q) for q in qs]
+    ids = _ids(T, topk, E, 22)
+    for call, seed in enumerate((23, 24)):
+        h = _hidden(T, H, seed).to(DEV)
+        inp, sc, out, *_rest = moe.quant_inp_act(h, ids.to(DEV), E, N, 1, qparams)
+        counts = _rest[3]
+        res = moe.gg_mxmoe_share_fused(inp, [w.B for w in ws], sc, [w.scale_b for w in ws], out, 2 * N, H, 2 * N, H,
+                                       qparams, counts)
+        assert res is out
+        torch.cuda.synchronize()
+        experts = [e for e in range(E) if int(counts[e]) > 0] + [E]
+        assert len(experts) == len(inp)
+        for pi, e in enumerate(experts):
+            w = ws[e]
+            A, sa = inp[pi].cpu().numpy(), sc[pi].cpu().numpy()
+            M = A.shape[0]
+            ref = oracle.gg_quant(A, w.B.cpu().numpy(), sa, w.scale_b.cpu().numpy(), M, w.N, w.K, w.q.a_bits)
+            got = out[pi].cpu().numpy()
+            assert (got.view(np.uint16) == ref.view(np.uint16)).all(), f"call {call} expert {e}"
+    assert len(moe._SHARE_FUSED_PLANS) >= 1
+
+
 def test_fast_quotient_matches_ieee_division():
     """moe_ops.hip div_f16_operands: q = x*r, q' = fma(fma(-q, s, x), r, q) with r = rcp(s) within
     1 ulp rounds to the same fp16 as the IEEE f32 quotient for fp16 x and s (the quantiser's

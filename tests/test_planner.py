@@ -101,10 +101,7 @@ def _xcd_queues(tiles):
     return q
 
 
-@pytest.mark.parametrize("placement", ["tail", "head"])
-def test_shared_expert_one_rectangle_per_xcd(monkeypatch, placement):
-    if placement == "head":
-        monkeypatch.setenv("MXMOE_GG_REGION", "1")
+def test_shared_expert_one_rectangle_per_xcd():
     shapes = _layer(8192)["gate_up"]  # the shared expert is the last problem: 32 x 44 tiles
     tiles, rows, v = check_coverage(shapes, nat.default_variant())
     shared = len(shapes) - 1
@@ -113,27 +110,41 @@ def test_shared_expert_one_rectangle_per_xcd(monkeypatch, placement):
         is_shared = [int(rows[t[0]]) == shared for t in q[x]]
         n = sum(is_shared)
         assert n == 32 * 44 // 8
-        if placement == "tail":  # the region closes the XCD's queue (default)
-            assert all(is_shared[-n:]) and not any(is_shared[:-n]), "region tiles must close the XCD queue"
-        else:
-            assert all(is_shared[:n]) and not any(is_shared[n:]), "region tiles must head the XCD queue"
+        # the region closes the XCD's queue
+        assert all(is_shared[-n:]) and not any(is_shared[:-n]), "region tiles must close the XCD queue"
         st = np.array([t for t, s in zip(q[x], is_shared) if s])
         m_panels, n_panels = len(np.unique(st[:, 1])), len(np.unique(st[:, 2]))
         # a rectangle: every (m, n) pair of its rows x columns
         assert m_panels * n_panels == n
         assert m_panels + n_panels <= 48  # 4 x 44 (vs 32 + 44 for a region of whole rows)
-    # A/B switch: without regions the shared expert is chunked across XCDs like any problem
-    monkeypatch.setenv("MXMOE_GG_REGION", "0")
-    tiles0, rows0 = nat.plan_tiles(_probs(shapes), v)
-    q0 = _xcd_queues(tiles0)
-    assert any(int(rows0[q0[x][-1][0]]) != shared for x in range(8)) or \
-        any(int(rows0[q0[x][0][0]]) != shared for x in range(8))
-    homes = collections.defaultdict(set)
-    for b, t in enumerate(tiles0):
-        if t[0] >= 0 and int(rows0[t[0]]) == shared:
-            homes[(t[1], t[2])].add(b % 8)
-    m_per_xcd = [len({m for (m, n), xs in homes.items() if x in xs}) for x in range(8)]
-    assert max(m_per_xcd) > 8  # chunked: every XCD sees most of the m-bands
+
+
+KNOBS = {"MXMOE_GG_BAND": "8", "MXMOE_GG_REGION": "1", "MXMOE_GG_REGION_ROT": "1", "MXMOE_GG_ALIGN": "0",
+         "MXMOE_GG_TAIL_CHUNK": "4", "MXMOE_GG_XCD_RR": "1"}
+
+
+@pytest.mark.parametrize("cfg", ["fp16", "w8a8"])
+def test_product_plan_ignores_planner_ab_switches(monkeypatch, cfg):
+    """The planner's A/B switches are read only by the tools-only lab library: the product
+    library's tile table does not depend on the caller's environment."""
+    kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym")}[cfg]
+    for gg in ("gate_up", "down"):
+        shapes = _layer(8192, **kw)[gg] + _layer(512, **kw)[gg]
+        probs = _probs(shapes)
+        v = nat.resolve_variant((nat.GGProblemC * len(probs))(*probs), len(probs), nat.VARIANT_AUTO)
+        base, rows = nat.plan_tiles(probs, v)
+        for k, val in KNOBS.items():
+            monkeypatch.setenv(k, val)
+        knobbed, rows2 = nat.plan_tiles(probs, v)
+        for k in KNOBS:
+            monkeypatch.delenv(k)
+        assert np.array_equal(base, knobbed) and np.array_equal(rows, rows2)
+
+
+def test_product_library_lists_only_correct_variants():
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    assert names and not any(n.startswith(("abl_", "x_")) for n in names)
+    assert nat.production_variants() == list(range(len(names)))
 
 
 def test_routed_experts_stay_on_one_xcd():

@@ -1,6 +1,7 @@
 """Weight-only WxA16 GroupGEMM on the GPU vs the oracle (fp16 tolerance of tests/_util.py)."""
 from __future__ import annotations
 
+import numpy as np
 import pytest
 import torch
 
@@ -53,3 +54,33 @@ def test_all_quant_types_in_one_launch(variant):
     gg.launch()
     torch.cuda.synchronize()
     _check(hps)
+
+
+@pytest.mark.parametrize("bs", [512, 128])
+def test_w4a16_w8a8_layer_bs512_matches_oracle(bs):
+    """BASELINE's small-batch mixed scheme (bench config w4a16_w8a8_bs512): the qwen2_moe layer-11
+    gate_up and down calls at bs = 512 with 1/16 of the blocks w8a8 and the rest w4a16_g-1_asym, ONE
+    fused AUTO launch each; every problem against the oracle on a row / column sample (w8a8 bit-exact,
+    w4a16 within the fp16 tolerance)."""
+    from mxmoe_amd.workload import load_workload, qwen2_layer11_workload, w4a16_w8a8_qconfig
+
+    layer = load_workload(qwen2_layer11_workload(bs, qconfig=w4a16_w8a8_qconfig()))["layer-11"]
+    rng = np.random.default_rng(bs)
+    for gg in ("gate_up", "down"):
+        shapes = layer[gg]
+        assert {s.qcfg for s in shapes} == {"w4a16_g-1_asym", "w8a8_g-1_sym"}
+        hps = [HostProblem(s.M, s.N, s.K, QParams(s.a_bits, s.w_bits, s.gsize, s.sym), seed=500 + i, device=DEV)
+               for i, s in enumerate(shapes)]
+        GroupGemm([h.problem for h in hps]).launch()
+        torch.cuda.synchronize()
+        for h in hps:
+            if h.M == 0:
+                continue
+            rows = np.unique(rng.integers(0, h.M, size=min(h.M, 16)))
+            cols = np.unique(rng.integers(0, h.N, size=24))
+            out = h.result()[np.ix_(rows, cols)]
+            ref = h.expected()[np.ix_(rows, cols)]
+            if h.q.is_weight_only:
+                assert_f16_close(out, ref, h.K)
+            else:
+                assert (out.view(np.uint16) == ref.view(np.uint16)).all(), f"{gg} w8a8 M={h.M}"
