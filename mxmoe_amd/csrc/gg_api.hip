@@ -237,6 +237,12 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | V2_BUF>("x_v2s_buf"),
       make_v2<V2_STAGGER | V2_BUF | (2 << V2_SPREAD_SHIFT)>("x_v2s_buf_spread2"),
       make_v2<V2_STAGGER | V2_BUF | (4 << V2_SPREAD_SHIFT)>("x_v2s_buf_spread4"),
+      make_v2<V2_STAGGER | V2_B3 | (2 << V2_SPREAD_SHIFT)>("x_v2s3_spread2"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | (2 << V2_SPREAD_SHIFT)>("x_v2s3_buf_spread2"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | (4 << V2_SPREAD_SHIFT)>("x_v2s3_buf_spread4"),
+      make_v2<V2_STAGGER | ABL_I4_FP6>("abl_v2s_i4_fp6"),
+      make_v2<V2_STAGGER | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s_spread2_stamp"),
+      make_v2<V2_STAGGER | V2_B3 | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_spread2_stamp"),
       // timing ablations of the staggered v2 (WRONG RESULTS by design; int8 tiles only)
       make_v2<V2_STAGGER | ABL_NO_DMA>("abl_v2s_nodma"),
       make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
@@ -1245,6 +1251,21 @@ int mxmoe_gg_debug_trace(void* dst, size_t bytes, int reset) {
   }
   return MXMOE_GG_OK;
 }
+
+#ifdef MXMOE_LAB
+// lab library only (not in include/mxmoe_gg.h): the spread mainloop's per-wave stage stamps
+int mxmoe_gg_debug_stamps(void* dst, size_t bytes, int reset) {
+  const size_t n = std::min(bytes, sizeof(g_gg_stamp));
+  if (dst && n) HIP_TRY(hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gg_stamp), n, 0, hipMemcpyDeviceToHost));
+  if (reset) {
+    void* p = nullptr;
+    HIP_TRY(hipGetSymbolAddress(&p, HIP_SYMBOL(g_gg_stamp)));
+    HIP_TRY(hipMemset(p, 0, sizeof(g_gg_stamp)));
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  return MXMOE_GG_OK;
+}
+#endif
 
 // Inverse of the reference's permute_weight(Row) + pack_weightonly (quantize.cuh:318-421), then
 // the kernel layout (include/mxmoe_gg.h). Host code, run once per weight at load time.

@@ -571,6 +571,11 @@ enum : int {
   // past num_records (the hardware returns zeros). Rows of a tile must span < 2 GiB (the planner
   // checks the row strides).
   V2_BUF = 1 << 21,
+  V2_STAMP = 1 << 22,  // diagnostics (lab only): s_memtime stamps around the spread loop's waits
+  // timing ablation (WRONG RESULTS by design; w4a4 tiles, staggered loop): each int4 half stage runs
+  // ONE v_mfma_scale_f32_16x16x128_f8f6f4 in FP6 (e2m3) format on the raw nibble words instead of two
+  // int8 MFMAs on widened nibbles: the upper bound of a w4a4 path on the FP6 MFMA (2x the int8 rate)
+  ABL_I4_FP6 = 1 << 23,
   // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
   // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
   ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
@@ -583,6 +588,12 @@ constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | AB
 // (100 MHz); read back with mxmoe_gg_debug_trace.
 constexpr int kTraceBlocks = 32768;
 __device__ uint64_t g_gg_trace[kTraceBlocks * 4];
+#ifdef MXMOE_LAB
+// per-wave stage stamps of the spread mainloop (V2_STAMP builds, lab library only): per (block, wave)
+// {sum of s_memtime cycles in the stage body, in the vmcnt(0) wait, in the barrier, steady stages}
+constexpr int kStampBlocks = 4096;
+__device__ uint64_t g_gg_stamp[kStampBlocks * 8 * 4];
+#endif
 __device__ __forceinline__ void trace_mark(int slot) {
   if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) g_gg_trace[blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
 }
@@ -609,7 +620,7 @@ __device__ __forceinline__ void v2_dma(const uint8_t* const (&src)[G], uint8_t* 
   }
 }
 
-template <class Cfg, int QT>
+template <class Cfg, int QT, int ABL = 0>
 struct V2Half {
   typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
   static constexpr int FM = Cfg::FM, FN = Cfg::FN;
@@ -633,6 +644,20 @@ struct V2Half {
     }
   }
   __device__ __forceinline__ void mma(typename AccT<QT>::type (&acc)[FM][FN]) const {
+    if constexpr (QT == QT_I4 && (ABL & ABL_I4_FP6) != 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const v8i aw = {a[0][i][0], a[0][i][1], a[1][i][0], a[1][i][1], a[0][i][0] ^ a[1][i][1], a[0][i][1], 0, 0};
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const v8i bw = {b[0][j][0], b[0][j][1], b[1][j][0], b[1][j][1], b[0][j][0] ^ b[1][j][1], b[0][j][1], 0, 0};
+          acc[i][j] = __builtin_bit_cast(
+              v4i, __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw, aw, __builtin_bit_cast(v4f, acc[i][j]), 2, 2, 0,
+                                                                    127, 0, 127));
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < SUBH; ++t) {
       if constexpr (QT == QT_I4) {
@@ -896,12 +921,194 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   // Waves 4-7 instead defer the second K half of every stage past the barrier, holding its
   // fragments in registers: after each barrier they start on MFMAs while waves 0-3 start on LDS
   // reads. Every accumulator still sees its K chunks in order -> bit-identical results.
-  if constexpr ((ABL & V2_STAGGER) != 0 && (ABL & V2_B3) != 0) {
+  if constexpr ((ABL & V2_STAGGER) != 0 && ((ABL >> V2_SPREAD_SHIFT) & 7) != 0) {
+    // Staggered v2 with the stage's LDS-DMA spread over the MFMAs. Each steady-state iteration (every
+    // piece it issues is a full 128-B stage) is one basic block, ordered by sched_group_barrier as
+    //   early waves: ds_read half 0 | {k MFMA, 1 DMA piece} x (GA+GB) | rest of half 0 | ds_read half 1 | MFMA half 1
+    //   late waves:  {1 DMA piece, k MFMA} x (GA+GB) | rest of the deferred half | ds_read | MFMA | ds_read
+    // then the stage-end wait + barrier. Two LDS images: v2s (both operands one stage ahead, two
+    // 64-KiB stages, vmcnt(0)) or, with V2_B3, v2s3 (A one stage ahead in a 2-stage ring, B two
+    // stages ahead in a 3-stage ring; the A pieces are issued first, so vmcnt(GB) leaves exactly
+    // B(s+2) in flight). The K-tail stages and the late waves' first stage run the plain bodies.
+    typedef V2Half<Cfg, QT, ABL> Half;
+    constexpr bool B3 = (ABL & V2_B3) != 0;
+    constexpr int NH = Half::kMfma, NR = Half::kReads, ND = GA + GB;
+    constexpr int KS0 = (ABL >> V2_SPREAD_SHIFT) & 7, KS = KS0 * ND <= NH ? KS0 : NH / ND;  // small tiles: denser
+    static_assert(KS >= 1, "spread: more DMA pieces than MFMAs in a half stage");
+    auto abuf = [&](int t) -> uint8_t* {
+      return B3 ? lds + (t & 1) * Cfg::A_BYTES : lds + (t & 1) * Cfg::STAGE_BYTES;
+    };
+    auto bbuf = [&](int t) -> uint8_t* {
+      return B3 ? lds + 2 * Cfg::A_BYTES + (t % 3) * Cfg::B_BYTES : lds + (t & 1) * Cfg::STAGE_BYTES + Cfg::A_BYTES;
+    };
+    // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select)
+    auto dma_a = [&](int t, bool full) {
+      const int kb = (ks0 + t) * Cfg::BKB, rsub = lane >> 3, p = lane & 7;
+      uint8_t* dst = abuf(t);
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const int kc = (p ^ ((((wave * GA + j) * 8 + rsub) >> 1) & 7)) << 4;
+        const bool in = full || kb + kc < kbytes;
+        if constexpr ((ABL & V2_BUF) != 0) bdma(rsA, in ? voA[j] : 0x80000000u, kb, dst + (wave * GA + j) * 1024);
+        else glds16(in ? srcA[j] + kb : reinterpret_cast<const uint8_t*>(g_zero16), dst + (wave * GA + j) * 1024);
+      }
+    };
+    auto dma_b = [&](int t, bool full) {
+      const int kb = (ks0 + t) * Cfg::BKB, rsub = lane >> 3, p = lane & 7;
+      uint8_t* dst = bbuf(t);
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int kc = (p ^ ((((wave * GB + j) * 8 + rsub) >> 1) & 7)) << 4;
+        const bool in = full || kb + kc < kbytes;
+        if constexpr ((ABL & V2_BUF) != 0) bdma(rsB, in ? voB[j] : 0x80000000u, kb, dst + (wave * GB + j) * 1024);
+        else glds16(in ? srcB[j] + kb : reinterpret_cast<const uint8_t*>(g_zero16), dst + (wave * GB + j) * 1024);
+      }
+    };
+    const int nst_full = (ks0 + nst) * Cfg::BKB > kbytes ? nst - 1 : nst;  // stages [0, nst_full) are full
+    auto full_stage = [&](int t) { return t < nst_full; };
+    // the pieces issued in iteration s (v2s: A(s+1), B(s+1); v2s3: A(s+1), B(s+2)), full stages only
+    auto dma_steady = [&](int s) {
+      dma_a(s + 1, true);
+      dma_b(s + (B3 ? 2 : 1), true);
+    };
+    auto dma_generic = [&](int s) {
+      if (s + 1 < nst) dma_a(s + 1, full_stage(s + 1));
+      const int tb = s + (B3 ? 2 : 1);
+      if (tb < nst) dma_b(tb, full_stage(tb));
+    };
+    // iterations s < nsteady issue only full stages
+    const int nsteady = nst_full - (B3 ? 2 : 1);
+    auto stage_wait = [&](int s) {  // stage s+1 landed (B3: B(s+2) may stay in flight)
+      if (B3 && s + 2 < nst) wait_vmcnt<GB>();
+      else wait_vmcnt<0>();
+    };
+    auto hread = [&](Half& f, int t, int h) { f.read(abuf(t), bbuf(t), a_row, b_row, swz, g, h); };
+    auto hmma = [&](const Half& f) { f.mma(acc); };
+    // V2_STAMP: body = loop top -> every MFMA issued (sched_barrier), vm = the stage-end vmcnt wait,
+    // bar = the barrier
+    [[maybe_unused]] auto stamped_sync = [&](int s, uint64_t t0, uint64_t& body, uint64_t& vm, uint64_t& bar) {
+      __builtin_amdgcn_sched_barrier(0);
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      stage_wait(s);
+      const uint64_t t2 = __builtin_amdgcn_s_memtime();
+      lds_barrier();
+      const uint64_t t3 = __builtin_amdgcn_s_memtime();
+      body += t1 - t0;
+      vm += t2 - t1;
+      bar += t3 - t2;
+    };
+    [[maybe_unused]] auto stamp_out = [&](uint64_t body, uint64_t vm, uint64_t bar, int n) {
+#ifdef MXMOE_LAB
+      if (lane == 0 && blockIdx.x < kStampBlocks && n > 0) {
+        uint64_t* o = g_gg_stamp + ((size_t)blockIdx.x * 8 + wave) * 4;
+        o[0] = body;
+        o[1] = vm;
+        o[2] = bar;
+        o[3] = (uint64_t)n;
+      }
+#endif
+    };
+    if (nst > 0) {
+      Half fr;
+      // prologue: stage 0 (and B3: B(1)) in flight, then the first barrier
+      dma_a(0, full_stage(0));
+      dma_b(0, full_stage(0));
+      if (B3 && nst > 1) dma_b(1, full_stage(1));
+      stage_wait(-1);
+      lds_barrier();
+      if constexpr (!B3) stash_scale();  // (B3: the rings fill the LDS, the stash follows the mainloop)
+      uint64_t st_body = 0, st_vm = 0, st_bar = 0;
+      if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
+        dma_generic(0);
+        hread(fr, 0, 0);
+        hmma(fr);
+        hread(fr, 0, 1);
+        stage_wait(0);
+        lds_barrier();
+        int s = 1;
+        for (; s < nsteady; ++s) {
+          [[maybe_unused]] uint64_t t0 = 0;
+          if constexpr ((ABL & V2_STAMP) != 0) t0 = __builtin_amdgcn_s_memtime();
+          dma_steady(s);
+          hmma(fr);  // second half of stage s-1
+          hread(fr, s, 0);
+          hmma(fr);
+          hread(fr, s, 1);
+#pragma unroll
+          for (int q = 0; q < ND; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          if constexpr ((ABL & V2_STAMP) != 0) {
+            stamped_sync(s, t0, st_body, st_vm, st_bar);
+          } else {
+            stage_wait(s);
+            lds_barrier();
+          }
+        }
+        if constexpr ((ABL & V2_STAMP) != 0) stamp_out(st_body, st_vm, st_bar, nsteady - 1);
+        for (; s < nst; ++s) {
+          dma_generic(s);
+          hmma(fr);
+          hread(fr, s, 0);
+          hmma(fr);
+          hread(fr, s, 1);
+          stage_wait(s);
+          lds_barrier();
+        }
+        hmma(fr);
+      } else {  // early waves
+        int s = 0;
+        for (; s < nsteady; ++s) {
+          [[maybe_unused]] uint64_t t0 = 0;
+          if constexpr ((ABL & V2_STAMP) != 0) t0 = __builtin_amdgcn_s_memtime();
+          hread(fr, s, 0);
+          dma_steady(s);
+          hmma(fr);
+          hread(fr, s, 1);
+          hmma(fr);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+          for (int q = 0; q < ND; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          if constexpr ((ABL & V2_STAMP) != 0) {
+            stamped_sync(s, t0, st_body, st_vm, st_bar);
+          } else {
+            stage_wait(s);
+            lds_barrier();
+          }
+        }
+        if constexpr ((ABL & V2_STAMP) != 0) stamp_out(st_body, st_vm, st_bar, nsteady);
+        for (; s < nst; ++s) {
+          dma_generic(s);
+          hread(fr, s, 0);
+          hmma(fr);
+          hread(fr, s, 1);
+          hmma(fr);
+          stage_wait(s);
+          lds_barrier();
+        }
+      }
+    }
+    if constexpr (B3) {
+      stash_scale();  // the rings are dead: the scale stash (past the epilogue image) is free
+      if constexpr (qt_scaled(QT)) __syncthreads();
+    }
+  } else if constexpr ((ABL & V2_STAGGER) != 0 && (ABL & V2_B3) != 0) {
     // B3: A ring of 2 stages at [0, 2 A_BYTES), B ring of 3 at [2 A_BYTES, + 3 B_BYTES). Stage s+1's
     // A and stage s+2's B are issued at the top of stage s; the barrier at its end waits for
     // everything but B(s+2) (issued last: vmcnt(GB)). A(s+1) refills the A buffer and B(s+2) the B
     // buffer stage s-1 was read from (every wave's reads of it completed before the last barrier).
-    typedef V2Half<Cfg, QT> Half;
+    typedef V2Half<Cfg, QT, ABL> Half;
     auto abuf = [&](int s) { return lds + (s & 1) * Cfg::A_BYTES; };
     auto bbuf = [&](int s) { return lds + 2 * Cfg::A_BYTES + (s % 3) * Cfg::B_BYTES; };
     auto issue_a = [&](int s) { v2_dma<GA>(srcA, abuf(s), (ks0 + s) * Cfg::BKB, kbytes, wave, lane); };
@@ -944,110 +1151,8 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
     stash_scale();  // the rings are dead: the scale stash (past the epilogue image) is free
     if constexpr (qt_scaled(QT)) __syncthreads();
-  } else if constexpr ((ABL & V2_STAGGER) != 0 && ((ABL >> V2_SPREAD_SHIFT) & 7) != 0) {
-    // staggered v2 with the stage's LDS-DMA spread over the MFMAs: the steady-state iterations
-    // (stage s+1 a full 128-B stage) are one basic block each, ordered by sched_group_barrier as
-    //   early waves: ds_read half 0 | {k MFMA, 1 DMA piece} x (GA+GB) | rest of half 0 | ds_read half 1 | MFMA half 1
-    //   late waves:  {1 DMA piece, k MFMA} x (GA+GB) | rest of the deferred half | ds_read | MFMA | ds_read
-    // then vmcnt(0) + barrier as v2s. The K-tail stage and the late waves' first stage run the v2s body.
-    typedef V2Half<Cfg, QT> Half;
-    constexpr int NH = Half::kMfma, NR = Half::kReads, ND = GA + GB;
-    constexpr int KS0 = (ABL >> V2_SPREAD_SHIFT) & 7, KS = KS0 * ND <= NH ? KS0 : NH / ND;  // small tiles: denser
-    static_assert(KS >= 1, "spread: more DMA pieces than MFMAs in a half stage");
-    auto hread = [&](Half& f, int buf, int h) {
-      f.read(lds + buf * Cfg::STAGE_BYTES, lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES, a_row, b_row, swz, g, h);
-    };
-    auto hmma = [&](const Half& f) { f.mma(acc); };
-    auto dma_full = [&](int t) {  // stage t (a full 128-B stage) into buffer t & 1
-      uint8_t* As = lds + (t & 1) * Cfg::STAGE_BYTES;
-      uint8_t* Bs = As + Cfg::A_BYTES;
-      const int kb = (ks0 + t) * Cfg::BKB;
-      if constexpr ((ABL & V2_BUF) != 0) {
-#pragma unroll
-        for (int j = 0; j < GA; ++j) bdma(rsA, voA[j], kb, As + (wave * GA + j) * 1024);
-#pragma unroll
-        for (int j = 0; j < GB; ++j) bdma(rsB, voB[j], kb, Bs + (wave * GB + j) * 1024);
-      } else {
-#pragma unroll
-        for (int j = 0; j < GA; ++j) glds16(srcA[j] + kb, As + (wave * GA + j) * 1024);
-#pragma unroll
-        for (int j = 0; j < GB; ++j) glds16(srcB[j] + kb, Bs + (wave * GB + j) * 1024);
-      }
-    };
-    auto sync = [&]() {
-      wait_vmcnt<0>();
-      lds_barrier();
-    };
-    const int nfull = nst - 1 - ((ks0 + nst) * Cfg::BKB > kbytes ? 1 : 0);  // iterations issuing a full stage
-    if (nst > 0) {
-      Half fr;
-      issue(0, 0);
-      __syncthreads();
-      stash_scale();
-      if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
-        if (nst > 1) issue(1, 1);
-        hread(fr, 0, 0);
-        hmma(fr);
-        hread(fr, 0, 1);
-        sync();
-        int s = 1;
-        for (; s < nfull; ++s) {
-          dma_full(s + 1);
-          hmma(fr);  // second half of stage s-1
-          hread(fr, s & 1, 0);
-          hmma(fr);
-          hread(fr, s & 1, 1);
-#pragma unroll
-          for (int q = 0; q < ND; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-          sync();
-        }
-        for (; s < nst; ++s) {
-          if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
-          hmma(fr);
-          hread(fr, s & 1, 0);
-          hmma(fr);
-          hread(fr, s & 1, 1);
-          sync();
-        }
-        hmma(fr);
-      } else {  // early waves
-        int s = 0;
-        for (; s < nfull; ++s) {
-          hread(fr, s & 1, 0);
-          dma_full(s + 1);
-          hmma(fr);
-          hread(fr, s & 1, 1);
-          hmma(fr);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-#pragma unroll
-          for (int q = 0; q < ND; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
-          sync();
-        }
-        for (; s < nst; ++s) {
-          if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
-          hread(fr, s & 1, 0);
-          hmma(fr);
-          hread(fr, s & 1, 1);
-          hmma(fr);
-          sync();
-        }
-      }
-    }
   } else if constexpr ((ABL & V2_STAGGER) != 0) {
-    typedef V2Half<Cfg, QT> Half;
+    typedef V2Half<Cfg, QT, ABL> Half;
     auto hread = [&](Half& f, int buf, int h) {
       f.read(lds + buf * Cfg::STAGE_BYTES, lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES, a_row, b_row, swz, g, h);
     };

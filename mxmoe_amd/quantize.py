@@ -92,15 +92,16 @@ E4M3_MAX = 448.0  # largest finite OCP e4m3 value
 
 def quant_e4m3(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """Per-row E4M3 quantisation of fp16 [rows, K] for w8a8_g-1_sym_E4M3 -> (uint8 OCP e4m3 codes in
-    logical K order, fp16 scales [rows]): scale = fp16(amax / 448) (0 -> 1), code = e4m3_rn(f32(x) /
-    f32(scale)), saturating. The reference defines the strategy (QCFG_W8A8_E4M3, tile_config.py:192)
+    logical K order, fp16 scales [rows]): scale = fp16(amax / 448), 1 for an all-zero row and at
+    least 2^-14 (the smallest normal fp16: a tiny row keeps nonzero codes instead of flushing to a
+    zero or subnormal scale), code = e4m3_rn(f32(x) / f32(scale)), saturating. The reference defines the strategy (QCFG_W8A8_E4M3, tile_config.py:192)
     but ships no quantiser for it; this is the natural per-channel analogue of quant_weight
     (quantize.cuh:218-279), restated in oracle/gg_oracle.c (oracle_quant_e4m3)."""
     if x.dtype != torch.float16:
         raise TypeError("quant_e4m3 expects fp16 input")
     amax = x.abs().amax(dim=-1).float()
-    scale = (amax / E4M3_MAX).half()
-    scale = torch.where(scale == 0, torch.ones_like(scale), scale)
+    scale = (amax / E4M3_MAX).half().clamp_min(2.0 ** -14)
+    scale = torch.where(amax == 0, torch.ones_like(scale), scale)
     q = (x.float() / scale.float()[:, None]).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
     return q.view(torch.uint8), scale
 

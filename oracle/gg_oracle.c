@@ -282,7 +282,8 @@ int oracle_quant_e4m3(const uint16_t* x, uint8_t* q, uint16_t* scale, int64_t ro
       if (v > mx) mx = v;
     }
     uint16_t s = oracle_f32_to_f16(mx / 448.0f);
-    if ((s & 0x7fff) == 0) s = 0x3c00;
+    if (mx == 0.0f) s = 0x3c00;           /* all-zero row: scale 1 */
+    else if (s < 0x0400) s = 0x0400;      /* at least the smallest normal fp16, 2^-14 */
     scale[r] = s;
     const float sf = oracle_f16_to_f32(s);
     for (int64_t k = 0; k < K; ++k) q[r * K + k] = oracle_f32_to_e4m3(oracle_f16_to_f32(x[r * K + k]) / sf);

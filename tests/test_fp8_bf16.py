@@ -51,11 +51,15 @@ def test_product_quantiser_matches_oracle_bit_exact():
     x = ((torch.rand(37, 272, generator=g) * 2 - 1) * torch.logspace(-4, 2, 37)[:, None]).half()
     x[3] = 0  # all-zero row: scale 1
     x[5, 7] = 60000.0  # large outlier row
+    x[9] = 0
+    x[9, 4], x[9, 100] = 1e-5, -3e-6  # tiny row: amax / 448 underflows fp16 -> scale 2^-14, codes kept
     q, s = quant_e4m3(x)
     qo, so = oracle.quant_e4m3(x.numpy())
     assert (s.numpy().view(np.uint16) == so.view(np.uint16)).all()
     assert (q.numpy() == qo).all()
     assert float(s[3]) == 1.0
+    assert float(s[9]) == 2.0 ** -14 and (q[9].numpy() != 0).sum() == 2
+    assert (s.float() >= 2.0 ** -14).all()
 
 
 def test_pack_e4m3_is_pack_wxax_byte_order():
