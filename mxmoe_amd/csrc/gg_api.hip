@@ -102,6 +102,7 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       case 4: launch_v2_q<ABL, 4>(a, grid, s); break;
       case 6: launch_v2_q<ABL, 6>(a, grid, s); break;
       case 8: launch_v2_q<ABL, 8>(a, grid, s); break;
+      case 128: launch_v2_q<ABL, 128>(a, grid, s); break;
       case 256: launch_v2_q<ABL, 256>(a, grid, s); break;
       default:
         fprintf(stderr, "libmxmoe_gg_lab: quant-type mix %#x not compiled in the lab build\n", qmask);
@@ -225,24 +226,23 @@ const std::vector<Variant>& variants() {
       make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
-      // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB): AUTO for short-K calls
+      // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB)
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
+      // round 3 (AUTO default): v2s3's LDS image, buffer-form LDS-DMA, the stage's pieces spread one
+      // per 4 MFMAs over the first MFMA group (profiles/r03/lab/)
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | (4 << V2_SPREAD_SHIFT)>("v2x_256x256_w8_b3_buf_spread4"),
 #else
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
       // mainloop experiments (correct results)
-      make_v2<V2_STAGGER | (1 << V2_SPREAD_SHIFT)>("x_v2s_spread1"),
-      make_v2<V2_STAGGER | (2 << V2_SPREAD_SHIFT)>("x_v2s_spread2"),
       make_v2<V2_STAGGER | (4 << V2_SPREAD_SHIFT)>("x_v2s_spread4"),
-      make_v2<V2_STAGGER | V2_BUF>("x_v2s_buf"),
-      make_v2<V2_STAGGER | V2_BUF | (2 << V2_SPREAD_SHIFT)>("x_v2s_buf_spread2"),
       make_v2<V2_STAGGER | V2_BUF | (4 << V2_SPREAD_SHIFT)>("x_v2s_buf_spread4"),
-      make_v2<V2_STAGGER | V2_B3 | (2 << V2_SPREAD_SHIFT)>("x_v2s3_spread2"),
-      make_v2<V2_STAGGER | V2_B3 | V2_BUF | (2 << V2_SPREAD_SHIFT)>("x_v2s3_buf_spread2"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | (4 << V2_SPREAD_SHIFT)>("x_v2s3_buf_spread4"),
-      make_v2<V2_STAGGER | ABL_I4_FP6>("abl_v2s_i4_fp6"),
-      make_v2<V2_STAGGER | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s_spread2_stamp"),
-      make_v2<V2_STAGGER | V2_B3 | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_spread2_stamp"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (2 << V2_SPREAD_SHIFT)>("x_v2s3_buf_edma2"),
+      make_v2<V2_STAGGER | V2_BUF | V2_EARLYDMA | (2 << V2_SPREAD_SHIFT)>("x_v2s_buf_edma2"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_edma2_stamp"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_STAMP | (4 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_sp4_stamp"),
+      make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
       // timing ablations of the staggered v2 (WRONG RESULTS by design; int8 tiles only)
       make_v2<V2_STAGGER | ABL_NO_DMA>("abl_v2s_nodma"),
       make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
@@ -262,16 +262,13 @@ const std::vector<Variant>& variants() {
   return v;
 }
 
-// AUTO policy (profiles/r01/kbench_*.jsonl, qwen2_moe layer 11): the staggered 256x256 v2 is the
-// fastest whenever fp16 or w8a8 problems are present; int4-only sets run 256x128 tiles, 2 WG/CU,
-// unless they are low-fill enough to need split-K (v2 kernels only).
-constexpr const char* kDefaultVariantName = "v2s_256x256_w8_dma_stagger";
+// AUTO policy: v2x (the staggered 256x256 v2 on v2s3's LDS image with the buffer-form, spread
+// LDS-DMA) for every call with fp16 / bf16 / w8a8 / E4M3 / weight-only problems: same-run A/B on the
+// qwen2_moe layer-11 calls, +5-11 % over v2s and +3-9 % over v2s3 at every K (the round-1/2 short-K
+// rule between those two is gone: profiles/r03/lab/). int4-only sets run 256x128 tiles, 2 WG/CU
+// (v3), unless they are low-fill enough to need split-K (v2 kernels only).
+constexpr const char* kDefaultVariantName = "v2x_256x256_w8_b3_buf_spread4";
 constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
-// short-K calls (median tile <= kShortKStages 128-B K stages, e.g. the qwen2_moe down GroupGEMM:
-// K = 1408): B two stages ahead pays for its 160-KiB LDS image (profiles/r01/session3, +3-5 % on
-// fp16 / w8a8 down, routed problems +7-9 %; +-1 % on gate_up, -1..3 % on dense 8192^3)
-constexpr const char* kShortKVariant = "v2s3_256x256_w8_dma_stagger_bring3";
-constexpr int kShortKStages = 24;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
@@ -780,33 +777,6 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     // to split K (that kernel cannot)
     Plan p;
     if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == 0) *out = variant_index(kInt4Variant);
-  } else if (mask & ((1 << QT_F16) | (1 << QT_I8) | (1 << QT_I4) | (1 << QT_F8) | (1 << QT_BF16))) {
-    std::vector<std::pair<int, int64_t>> st;  // (128-B K stages, tiles) of the fp16 / w8a8 / w4a4 problems
-    int64_t total = 0, f16_small = 0;         // f16_small: fp16 tiles of the 64-row class
-    for (const HostProblem& p : hp) {
-      int qt;
-      if (p.M <= 0 || qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt, &qt) != MXMOE_GG_OK) continue;
-      if (qt != QT_F16 && qt != QT_I8 && qt != QT_I4 && qt != QT_F8 && qt != QT_BF16) continue;
-      const int64_t nt = (p.N + 255) / 256, tiles = (int64_t)((p.M + 255) / 256) * nt;
-      st.emplace_back((int)(((int64_t)p.K * p.a_bits / 8 + 127) / 128), tiles);
-      total += tiles;
-      if (is_float16(qt) && p.M % 256 > 0 && p.M % 256 <= 64) f16_small += nt;
-    }
-    // low-fill fp16 calls (most tiles are 64-row remainders, e.g. bs=512 routed experts): those
-    // tiles wait on their B stream, and the deeper B ring pays (+5-9 %, session3/exp_b3_bs512.jsonl)
-    if (total > 0 && 2 * f16_small >= total) {
-      *out = variant_index(kShortKVariant);
-      return MXMOE_GG_OK;
-    }
-    std::sort(st.begin(), st.end());
-    int64_t acc = 0;
-    for (const auto& e : st) {
-      acc += e.second;
-      if (2 * acc >= total) {
-        if (e.first <= kShortKStages) *out = variant_index(kShortKVariant);
-        break;
-      }
-    }
   }
   return MXMOE_GG_OK;
 }

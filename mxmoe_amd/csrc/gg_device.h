@@ -576,6 +576,14 @@ enum : int {
   // ONE v_mfma_scale_f32_16x16x128_f8f6f4 in FP6 (e2m3) format on the raw nibble words instead of two
   // int8 MFMAs on widened nibbles: the upper bound of a w4a4 path on the FP6 MFMA (2x the int8 rate)
   ABL_I4_FP6 = 1 << 23,
+  // spread option: the A pieces go one per NH/GA MFMAs of the first MFMA group, the B pieces one per
+  // NH/GB MFMAs of the second (v2s3: B(s+2) has a whole stage more to land)
+  V2_SPLITAB = 1 << 24,
+  // spread + buffer-form option: waves 0-3 issue every LDS-DMA piece of the workgroup (their own and
+  // their SIMD partner w+4's), waves 4-7 none — the stamps show the late waves are the stage's
+  // critical path while the early ones wait ~1000 cycles at the barrier. Rows past M / N are read
+  // out of the buffer's range (zeros) instead of clamped.
+  V2_EARLYDMA = 1 << 25,
   // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
   // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
   ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
@@ -732,22 +740,26 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     }
   }
   // V2_BUF: per-tile buffer resources and fixed 32-bit lane offsets (rows relative to m0 / n0)
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(A) + (int64_t)m0 * lda, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B) + (int64_t)n0 * ldb, (short)0, 0x7fffffff, 0x00020000);
+  // (V2_EARLYDMA: num_records ends at row M / N, rows past it read as zeros; else rows are clamped)
+  constexpr bool kOobRows = (ABL & V2_EARLYDMA) != 0;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(A) + (int64_t)m0 * lda, (short)0,
+      kOobRows ? (int)(min(M - m0, Cfg::BM) * lda) : 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(B) + (int64_t)n0 * ldb, (short)0,
+      kOobRows ? (int)(min(N - n0, Cfg::BN) * ldb) : 0x7fffffff, 0x00020000);
   uint32_t voA[GA], voB[GB];
   {
     const int rsub = lane >> 3, p = lane & 7;
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
       const int row = (wave * GA + j) * 8 + rsub;
-      voA[j] = (uint32_t)((min(m0 + row, M - 1) - m0) * lda) + ((p ^ ((row >> 1) & 7)) << 4);
+      voA[j] = (uint32_t)((kOobRows ? row : min(m0 + row, M - 1) - m0) * lda) + ((p ^ ((row >> 1) & 7)) << 4);
     }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const int row = (wave * GB + j) * 8 + rsub;
-      voB[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb) + ((p ^ ((row >> 1) & 7)) << 4);
+      voB[j] = (uint32_t)((kOobRows ? row : min(n0 + row, N - 1) - n0) * ldb) + ((p ^ ((row >> 1) & 7)) << 4);
     }
   }
   auto bdma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t vo, int kb, uint8_t* dst) {
@@ -935,6 +947,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     constexpr int NH = Half::kMfma, NR = Half::kReads, ND = GA + GB;
     constexpr int KS0 = (ABL >> V2_SPREAD_SHIFT) & 7, KS = KS0 * ND <= NH ? KS0 : NH / ND;  // small tiles: denser
     static_assert(KS >= 1, "spread: more DMA pieces than MFMAs in a half stage");
+    constexpr int KSA = NH / GA, KSB = NH / GB;  // V2_SPLITAB: A pieces over group 1, B over group 2
     auto abuf = [&](int t) -> uint8_t* {
       return B3 ? lds + (t & 1) * Cfg::A_BYTES : lds + (t & 1) * Cfg::STAGE_BYTES;
     };
@@ -942,46 +955,70 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       return B3 ? lds + 2 * Cfg::A_BYTES + (t % 3) * Cfg::B_BYTES : lds + (t & 1) * Cfg::STAGE_BYTES + Cfg::A_BYTES;
     };
     // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select)
-    auto dma_a = [&](int t, bool full) {
+    constexpr bool EDMA = (ABL & V2_EARLYDMA) != 0;
+    static_assert(!EDMA || (ABL & V2_BUF) != 0, "V2_EARLYDMA needs the buffer-form DMA");
+    constexpr int HALFW = Cfg::WM * Cfg::WN / 2;  // SIMD partner of wave w is w + HALFW
+    // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select).
+    // EDMA: early waves issue their partner's pieces too (rows + 8 * G * HALFW, the same swizzle),
+    // late waves none; `early` is a constant after inlining into either wave's loop.
+    auto dma_a = [&](int t, bool full, bool early) {
       const int kb = (ks0 + t) * Cfg::BKB, rsub = lane >> 3, p = lane & 7;
       uint8_t* dst = abuf(t);
+      if (EDMA && !early) return;
 #pragma unroll
-      for (int j = 0; j < GA; ++j) {
-        const int kc = (p ^ ((((wave * GA + j) * 8 + rsub) >> 1) & 7)) << 4;
-        const bool in = full || kb + kc < kbytes;
-        if constexpr ((ABL & V2_BUF) != 0) bdma(rsA, in ? voA[j] : 0x80000000u, kb, dst + (wave * GA + j) * 1024);
-        else glds16(in ? srcA[j] + kb : reinterpret_cast<const uint8_t*>(g_zero16), dst + (wave * GA + j) * 1024);
+      for (int w2 = 0; w2 < (EDMA ? 2 : 1); ++w2) {
+        const int ww = wave + w2 * HALFW;
+        const uint32_t radd = (uint32_t)(w2 * 8 * GA * HALFW * lda);
+#pragma unroll
+        for (int j = 0; j < GA; ++j) {
+          const int kc = (p ^ ((((wave * GA + j) * 8 + rsub) >> 1) & 7)) << 4;
+          const bool in = full || kb + kc < kbytes;
+          if constexpr ((ABL & V2_BUF) != 0) bdma(rsA, in ? voA[j] + radd : 0x80000000u, kb, dst + (ww * GA + j) * 1024);
+          else glds16(in ? srcA[j] + kb : reinterpret_cast<const uint8_t*>(g_zero16), dst + (wave * GA + j) * 1024);
+        }
       }
     };
-    auto dma_b = [&](int t, bool full) {
+    auto dma_b = [&](int t, bool full, bool early) {
       const int kb = (ks0 + t) * Cfg::BKB, rsub = lane >> 3, p = lane & 7;
       uint8_t* dst = bbuf(t);
+      if (EDMA && !early) return;
 #pragma unroll
-      for (int j = 0; j < GB; ++j) {
-        const int kc = (p ^ ((((wave * GB + j) * 8 + rsub) >> 1) & 7)) << 4;
-        const bool in = full || kb + kc < kbytes;
-        if constexpr ((ABL & V2_BUF) != 0) bdma(rsB, in ? voB[j] : 0x80000000u, kb, dst + (wave * GB + j) * 1024);
-        else glds16(in ? srcB[j] + kb : reinterpret_cast<const uint8_t*>(g_zero16), dst + (wave * GB + j) * 1024);
+      for (int w2 = 0; w2 < (EDMA ? 2 : 1); ++w2) {
+        const int ww = wave + w2 * HALFW;
+        const uint32_t radd = (uint32_t)(w2 * 8 * GB * HALFW * ldb);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+          const int kc = (p ^ ((((wave * GB + j) * 8 + rsub) >> 1) & 7)) << 4;
+          const bool in = full || kb + kc < kbytes;
+          if constexpr ((ABL & V2_BUF) != 0) bdma(rsB, in ? voB[j] + radd : 0x80000000u, kb, dst + (ww * GB + j) * 1024);
+          else glds16(in ? srcB[j] + kb : reinterpret_cast<const uint8_t*>(g_zero16), dst + (wave * GB + j) * 1024);
+        }
       }
     };
     const int nst_full = (ks0 + nst) * Cfg::BKB > kbytes ? nst - 1 : nst;  // stages [0, nst_full) are full
     auto full_stage = [&](int t) { return t < nst_full; };
     // the pieces issued in iteration s (v2s: A(s+1), B(s+1); v2s3: A(s+1), B(s+2)), full stages only
-    auto dma_steady = [&](int s) {
-      dma_a(s + 1, true);
-      dma_b(s + (B3 ? 2 : 1), true);
+    auto dma_steady = [&](int s, bool early) {
+      dma_a(s + 1, true, early);
+      dma_b(s + (B3 ? 2 : 1), true, early);
     };
-    auto dma_generic = [&](int s) {
-      if (s + 1 < nst) dma_a(s + 1, full_stage(s + 1));
+    auto dma_generic = [&](int s, bool early) {
+      if (s + 1 < nst) dma_a(s + 1, full_stage(s + 1), early);
       const int tb = s + (B3 ? 2 : 1);
-      if (tb < nst) dma_b(tb, full_stage(tb));
+      if (tb < nst) dma_b(tb, full_stage(tb), early);
     };
     // iterations s < nsteady issue only full stages
     const int nsteady = nst_full - (B3 ? 2 : 1);
     auto stage_wait = [&](int s) {  // stage s+1 landed (B3: B(s+2) may stay in flight)
-      if (B3 && s + 2 < nst) wait_vmcnt<GB>();
+      if (B3 && s + 2 < nst) wait_vmcnt<(EDMA ? 2 : 1) * GB>();
       else wait_vmcnt<0>();
     };
+    // EDMA: the early waves carry twice the pieces, the late ones none
+    // (64-row tiles: more pieces than MFMAs in a half stage -> one MFMA per piece, the rest of the
+    // pieces run into the second group)
+    constexpr int NDE = EDMA ? 2 * ND : ND;
+    constexpr int KSE = KS0 * NDE <= NH ? KS0 : (NH / NDE > 0 ? NH / NDE : 1);
+    constexpr int RESTE = NH - KSE * NDE > 0 ? NH - KSE * NDE : 0;
     auto hread = [&](Half& f, int t, int h) { f.read(abuf(t), bbuf(t), a_row, b_row, swz, g, h); };
     auto hmma = [&](const Half& f) { f.mma(acc); };
     // V2_STAMP: body = loop top -> every MFMA issued (sched_barrier), vm = the stage-end vmcnt wait,
@@ -1011,15 +1048,16 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     if (nst > 0) {
       Half fr;
       // prologue: stage 0 (and B3: B(1)) in flight, then the first barrier
-      dma_a(0, full_stage(0));
-      dma_b(0, full_stage(0));
-      if (B3 && nst > 1) dma_b(1, full_stage(1));
+      const bool early_w = wave < HALFW;
+      dma_a(0, full_stage(0), early_w);
+      dma_b(0, full_stage(0), early_w);
+      if (B3 && nst > 1) dma_b(1, full_stage(1), early_w);
       stage_wait(-1);
       lds_barrier();
       if constexpr (!B3) stash_scale();  // (B3: the rings fill the LDS, the stash follows the mainloop)
       uint64_t st_body = 0, st_vm = 0, st_bar = 0;
       if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
-        dma_generic(0);
+        dma_generic(0, false);
         hread(fr, 0, 0);
         hmma(fr);
         hread(fr, 0, 1);
@@ -1029,20 +1067,42 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         for (; s < nsteady; ++s) {
           [[maybe_unused]] uint64_t t0 = 0;
           if constexpr ((ABL & V2_STAMP) != 0) t0 = __builtin_amdgcn_s_memtime();
-          dma_steady(s);
+          dma_steady(s, false);
           hmma(fr);  // second half of stage s-1
           hread(fr, s, 0);
           hmma(fr);
           hread(fr, s, 1);
+          if constexpr (EDMA) {
+            __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          } else if constexpr ((ABL & V2_SPLITAB) != 0) {
 #pragma unroll
-          for (int q = 0; q < ND; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+            for (int q = 0; q < GA; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, KSA, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NH - KSA * GA, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+            for (int q = 0; q < GB; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, KSB, 0);
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NH - KSB * GB, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          } else {
+#pragma unroll
+            for (int q = 0; q < ND; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
           }
-          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
           if constexpr ((ABL & V2_STAMP) != 0) {
             stamped_sync(s, t0, st_body, st_vm, st_bar);
           } else {
@@ -1052,7 +1112,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         }
         if constexpr ((ABL & V2_STAMP) != 0) stamp_out(st_body, st_vm, st_bar, nsteady - 1);
         for (; s < nst; ++s) {
-          dma_generic(s);
+          dma_generic(s, false);
           hmma(fr);
           hread(fr, s, 0);
           hmma(fr);
@@ -1067,19 +1127,44 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           [[maybe_unused]] uint64_t t0 = 0;
           if constexpr ((ABL & V2_STAMP) != 0) t0 = __builtin_amdgcn_s_memtime();
           hread(fr, s, 0);
-          dma_steady(s);
+          dma_steady(s, true);
           hmma(fr);
           hread(fr, s, 1);
           hmma(fr);
           __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          if constexpr (EDMA) {
 #pragma unroll
-          for (int q = 0; q < ND; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            for (int q = 0; q < NDE; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, KSE, 0);
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, RESTE, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          } else if constexpr ((ABL & V2_SPLITAB) != 0) {
+#pragma unroll
+            for (int q = 0; q < GA; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, KSA, 0);
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NH - KSA * GA, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+            for (int q = 0; q < GB; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, KSB, 0);
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NH - KSB * GB, 0);
+          } else {
+#pragma unroll
+            for (int q = 0; q < ND; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
           }
-          __builtin_amdgcn_sched_group_barrier(0x008, NH - KS * ND, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
           if constexpr ((ABL & V2_STAMP) != 0) {
             stamped_sync(s, t0, st_body, st_vm, st_bar);
           } else {
@@ -1089,7 +1174,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         }
         if constexpr ((ABL & V2_STAMP) != 0) stamp_out(st_body, st_vm, st_bar, nsteady);
         for (; s < nst; ++s) {
-          dma_generic(s);
+          dma_generic(s, true);
           hread(fr, s, 0);
           hmma(fr);
           hread(fr, s, 1);

@@ -73,7 +73,7 @@ def test_auto_variant_follows_quant_mix():
         arr = (nat.GGProblemC * len(ps))(*ps)
         return nat.workspace_size(arr, len(ps), v)
 
-    assert names[nat.default_variant()] == "v2s_256x256_w8_dma_stagger"
+    assert names[nat.default_variant()] == "v2x_256x256_w8_b3_buf_spread4"
     big = dict(M=4096, N=4096, K=1024)
     w8 = [_prob(**big)]
     w4 = [_prob(a_bits=4, w_bits=4, **big)] * 2
@@ -85,33 +85,24 @@ def test_auto_variant_follows_quant_mix():
     assert ws(w4 + [_prob(M=0)], nat.VARIANT_AUTO) == ws(w4 + [_prob(M=0)], int4_v)
 
 
-def test_auto_variant_short_k_rule():
-    """AUTO: median tile <= 24 128-B K stages -> the 3-stage-B-ring kernel; longer K -> the default."""
-    names = [ln.split()[1] for ln in nat.list_variants()]
-    b3 = names.index("v2s3_256x256_w8_dma_stagger_bring3")
-
+def test_auto_variant_is_v2x_at_every_k():
+    """AUTO (round 3): every call with fp16 / int8 problems runs v2x, at short and long K alike (v2x
+    carries the 3-stage B ring that round 2's short-K rule chose v2s3 for)."""
     def auto(ps):
         arr = (nat.GGProblemC * len(ps))(*ps)
         return nat.resolve_variant(arr, len(ps))
 
     f16 = dict(a_bits=16, w_bits=16, scale_a=0, scale_b=0)
-    assert auto([_prob(M=4096, N=4096, K=2048, **f16)]) == nat.default_variant()  # 32 stages
-    assert auto([_prob(M=4096, N=4096, K=1408, **f16)]) == b3  # 22 stages
-    assert auto([_prob(M=4096, N=4096, K=2048)]) == b3  # int8: 16 stages
-    assert auto([_prob(M=4096, N=4096, K=4096)]) == nat.default_variant()  # int8: 32 stages
-    # the median is tile-weighted: one big long-K problem outweighs several small short-K ones
-    assert auto([_prob(M=8192, N=8192, K=4096, **f16)] + [_prob(M=256, N=256, K=256, **f16)] * 4) == \
-        nat.default_variant()
+    for K in (256, 1408, 2048, 4096):
+        assert auto([_prob(M=4096, N=4096, K=K, **f16)]) == nat.default_variant()
+        assert auto([_prob(M=4096, N=4096, K=K)]) == nat.default_variant()
     from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
 
-    layer = load_workload(qwen2_layer11_workload(8192))["layer-11"]
-    for gg, want in (("gate_up", nat.default_variant()), ("down", b3)):
-        probs = [_prob(M=s.M, N=s.N, K=s.K, **f16) for s in layer[gg]]
-        assert auto(probs) == want, gg
-    assert auto([_prob(M=64, N=128, K=256)]) == nat.resolve_variant((nat.GGProblemC * 1)(_prob(M=64, N=128, K=256)), 1, b3)
-    # low-fill fp16 (bs=512: most tiles are 64-row remainders) -> the deep B ring even at long K
-    small = load_workload(qwen2_layer11_workload(512))["layer-11"]["gate_up"]
-    assert auto([_prob(M=s.M, N=s.N, K=s.K, **f16) for s in small]) == b3
+    for bs in (8192, 512):
+        layer = load_workload(qwen2_layer11_workload(bs))["layer-11"]
+        for gg in ("gate_up", "down"):
+            probs = [_prob(M=s.M, N=s.N, K=s.K, **f16) for s in layer[gg]]
+            assert auto(probs) == nat.default_variant(), (bs, gg)
 
 
 def _plan(problems, ws_bytes=1 << 20):
