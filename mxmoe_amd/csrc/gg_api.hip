@@ -228,9 +228,10 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
       // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB)
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
-      // round 3 (AUTO default): v2s3's LDS image, buffer-form LDS-DMA, the stage's pieces spread one
-      // per 4 MFMAs over the first MFMA group (profiles/r03/lab/)
-      make_v2<V2_STAGGER | V2_B3 | V2_BUF | (4 << V2_SPREAD_SHIFT)>("v2x_256x256_w8_b3_buf_spread4"),
+      // round 3 (AUTO default): v2s3's LDS image, buffer-form LDS-DMA spread over the first MFMA
+      // group of each half stage, issued by waves 0-3 for their SIMD partners too (not on int4
+      // tiles) — profiles/r03/lab/
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT)>("v2x_256x256_w8_b3_buf_spread_edma"),
 #else
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
@@ -240,6 +241,9 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | (4 << V2_SPREAD_SHIFT)>("x_v2s3_buf_spread4"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (2 << V2_SPREAD_SHIFT)>("x_v2s3_buf_edma2"),
       make_v2<V2_STAGGER | V2_BUF | V2_EARLYDMA | (2 << V2_SPREAD_SHIFT)>("x_v2s_buf_edma2"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT)>("x_v2s3_buf_edma4"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_TRACE | (4 << V2_SPREAD_SHIFT)>("abl_v2x_trace"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_TRACE | (2 << V2_SPREAD_SHIFT)>("abl_v2x_edma_trace"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_edma2_stamp"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_STAMP | (4 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_sp4_stamp"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
@@ -267,7 +271,7 @@ const std::vector<Variant>& variants() {
 // qwen2_moe layer-11 calls, +5-11 % over v2s and +3-9 % over v2s3 at every K (the round-1/2 short-K
 // rule between those two is gone: profiles/r03/lab/). int4-only sets run 256x128 tiles, 2 WG/CU
 // (v3), unless they are low-fill enough to need split-K (v2 kernels only).
-constexpr const char* kDefaultVariantName = "v2x_256x256_w8_b3_buf_spread4";
+constexpr const char* kDefaultVariantName = "v2x_256x256_w8_b3_buf_spread_edma";
 constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 

@@ -584,6 +584,9 @@ enum : int {
   // critical path while the early ones wait ~1000 cycles at the barrier. Rows past M / N are read
   // out of the buffer's range (zeros) instead of clamped.
   V2_EARLYDMA = 1 << 25,
+  // spread option: static priority 1 for the late waves (4-7) through the mainloop — the stamps put
+  // them on the stage's critical path, the early waves wait ~1000 cycles at every barrier
+  V2_PRIO_LATE = 1 << 26,
   // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
   // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
   ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
@@ -955,7 +958,9 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       return B3 ? lds + 2 * Cfg::A_BYTES + (t % 3) * Cfg::B_BYTES : lds + (t & 1) * Cfg::STAGE_BYTES + Cfg::A_BYTES;
     };
     // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select)
-    constexpr bool EDMA = (ABL & V2_EARLYDMA) != 0;
+    // (not on int4 tiles: their half stages carry twice the MFMAs, the early waves have no slack —
+    //  w4a4 2.5-4.3 % slower with it, profiles/r03/lab/lab_r3.jsonl)
+    constexpr bool EDMA = (ABL & V2_EARLYDMA) != 0 && QT != QT_I4;
     static_assert(!EDMA || (ABL & V2_BUF) != 0, "V2_EARLYDMA needs the buffer-form DMA");
     constexpr int HALFW = Cfg::WM * Cfg::WN / 2;  // SIMD partner of wave w is w + HALFW
     // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select).
@@ -1057,6 +1062,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       if constexpr (!B3) stash_scale();  // (B3: the rings fill the LDS, the stash follows the mainloop)
       uint64_t st_body = 0, st_vm = 0, st_bar = 0;
       if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
+        if constexpr ((ABL & V2_PRIO_LATE) != 0) __builtin_amdgcn_s_setprio(1);
         dma_generic(0, false);
         hread(fr, 0, 0);
         hmma(fr);
@@ -1121,6 +1127,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           lds_barrier();
         }
         hmma(fr);
+        if constexpr ((ABL & V2_PRIO_LATE) != 0) __builtin_amdgcn_s_setprio(0);
       } else {  // early waves
         int s = 0;
         for (; s < nsteady; ++s) {

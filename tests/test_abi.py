@@ -73,7 +73,7 @@ def test_auto_variant_follows_quant_mix():
         arr = (nat.GGProblemC * len(ps))(*ps)
         return nat.workspace_size(arr, len(ps), v)
 
-    assert names[nat.default_variant()] == "v2x_256x256_w8_b3_buf_spread4"
+    assert names[nat.default_variant()] == "v2x_256x256_w8_b3_buf_spread_edma"
     big = dict(M=4096, N=4096, K=1024)
     w8 = [_prob(**big)]
     w4 = [_prob(a_bits=4, w_bits=4, **big)] * 2

@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--dense", default="")
     ap.add_argument("--dump", default="")
     ap.add_argument("--env", default="", help="KEY=VALUE set before planning (e.g. MXMOE_GG_XCD_BALANCE=0)")
+    ap.add_argument("--variant-name", default="abl_v2s_trace", help="a V2_TRACE build of the lab library")
     args = ap.parse_args()
     if args.env:
         k, v = args.env.split("=", 1)
@@ -102,15 +103,14 @@ def main():
     else:
         shapes = load_workload(qwen2_layer11_workload(args.bs, **kw))["layer-11"][args.gg]
     inp = build_layer_inputs(shapes)
-    trace_v = nat.variant_index("abl_v2s_trace") if hasattr(nat, "variant_index") else \
-        [l.split()[1] for l in nat.list_variants()].index("abl_v2s_trace")
+    trace_v = [ln.split()[1] for ln in nat.list_variants()].index(args.variant_name)
     gg = GroupGemm(inp.problems, variant=trace_v)
     t = time_launches(gg.launch, warmup=20, iters=50)
     fetch(0, reset=True)
     gg.launch()
     torch.cuda.synchronize()
     tr = fetch(gg.info.grid, reset=False)
-    res = {"cfg": args.cfg, "gg": args.dense or args.gg, "bs": args.bs, "env": args.env, "event_median_ms": round(t["median_ms"], 4)}
+    res = {"variant": args.variant_name, "cfg": args.cfg, "gg": args.dense or args.gg, "bs": args.bs, "env": args.env, "event_median_ms": round(t["median_ms"], 4)}
     res.update(analyse(tr))
     print(json.dumps(res), flush=True)
     if args.dump:
