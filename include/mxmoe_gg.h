@@ -106,6 +106,9 @@ typedef struct mxmoe_gg_plan_info {
   int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */
   void* workspace;         /* device workspace the plan was written to */
   uint64_t signature;      /* hash of the plan table and tile table (shapes, quant params, strides) */
+  int32_t tile_slots;      /* entries of the device tile table (= grid, except for persistent variants,
+                            * whose workgroups walk [k][grid]-ordered tile lists) */
+  int32_t reserved;
 } mxmoe_gg_plan_info;
 
 int mxmoe_gg_abi_version(void);

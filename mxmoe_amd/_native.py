@@ -70,7 +70,7 @@ class GGPlanInfo(ctypes.Structure):
         ("variant", ctypes.c_int32), ("problem_count", ctypes.c_int32), ("total_tiles", ctypes.c_int32),
         ("grid", ctypes.c_int32), ("block", ctypes.c_int32), ("lds_bytes", ctypes.c_int32),
         ("qtype_mask", ctypes.c_int32), ("splitk_slabs", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64), ("workspace", ctypes.c_void_p),
-        ("signature", ctypes.c_uint64),
+        ("signature", ctypes.c_uint64), ("tile_slots", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
 

@@ -75,6 +75,7 @@ struct Variant {
   int k_stage_bytes;   // K bytes per row must be a multiple of this (0 = any multiple of 16)
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
   int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
+  bool persistent = false;  // v2p: one workgroup per CU walks a planned tile list
   void (*launch)(const GGArgs&, int grid, int qmask, hipStream_t);  // qmask: 1 << QType present
 };
 
@@ -152,6 +153,20 @@ void launch_v3(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   }
 }
 
+template <int QM, int TRACE>
+void launch_v2p_q(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gg_v2p_kernel<QM, TRACE>), dim3(grid), dim3(512), 0, s, a);
+}
+template <int TRACE = 0>
+void launch_v2p(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  switch (qmask & 511) {
+    case 1: launch_v2p_q<1, TRACE>(a, grid, s); break;
+    case 2: launch_v2p_q<2, TRACE>(a, grid, s); break;
+    case 256: launch_v2p_q<256, TRACE>(a, grid, s); break;
+    default: launch_v2p_q<511, TRACE>(a, grid, s); break;  // every tile body
+  }
+}
+
 template <class C16, class C8, class C4>
 Variant make_v0(const char* name) {
   Variant v;
@@ -208,6 +223,15 @@ Variant make_v2(const char* name) {
 }
 
 
+template <int TRACE = 0>
+Variant make_v2p(const char* name) {
+  Variant v = make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT)>(name);
+  v.persistent = true;
+  v.lds_bytes = 160 * 1024;
+  v.launch = &launch_v2p<TRACE>;
+  return v;
+}
+
 typedef TileCfg<128, 128, 2, 2, 2> T128x128;
 typedef TileCfg<256, 128, 2, 2, 1> T256x128;
 typedef TileCfg<128, 256, 2, 2, 1> T128x256;
@@ -242,6 +266,8 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (2 << V2_SPREAD_SHIFT)>("x_v2s3_buf_edma2"),
       make_v2<V2_STAGGER | V2_BUF | V2_EARLYDMA | (2 << V2_SPREAD_SHIFT)>("x_v2s_buf_edma2"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT)>("x_v2s3_buf_edma4"),
+      make_v2p("x_v2p_256x256_w8_persistent"),
+      make_v2p<1>("abl_v2p_trace"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_TRACE | (4 << V2_SPREAD_SHIFT)>("abl_v2x_trace"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_TRACE | (2 << V2_SPREAD_SHIFT)>("abl_v2x_edma_trace"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_edma2_stamp"),
@@ -451,6 +477,7 @@ struct Plan {
   std::vector<int> order;       // table row -> caller's problem index
   std::vector<TileDesc> tiles;  // indexed by blockIdx
   int total_tiles = 0;
+  int launch_grid = 0;          // workgroups launched (= tiles.size() unless persistent)
   int slabs = 0;                // split-K partial slabs
 };
 
@@ -755,6 +782,33 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     }
   plan->tiles.resize(grid);
   plan->total_tiles = T;
+  plan->launch_grid = grid;
+  if (v.persistent) {
+    // v2p: each XCD's queue handed out to its `chunk` workgroups in queue order, every tile to the
+    // workgroup whose modelled finish is earliest (what the hardware's dispatch does with blocks,
+    // planned once here); workgroup w = 8 * slot + x sits on XCD x under round-robin placement
+    // (speed only). Table [k][G] with a terminating row of empty slots.
+    const int G = 8 * chunk;
+    std::vector<std::vector<int>> lists(G);
+    for (int x = 0; x < 8; ++x) {
+      std::vector<std::pair<double, int>> heap;
+      for (int sl = 0; sl < chunk; ++sl) heap.push_back({0.0, sl});
+      std::make_heap(heap.begin(), heap.end(), std::greater<std::pair<double, int>>());
+      for (int idx : queue[x]) {
+        std::pop_heap(heap.begin(), heap.end(), std::greater<std::pair<double, int>>());
+        auto& top = heap.back();
+        lists[8 * top.second + x].push_back(idx);
+        top.first += tile_time(all_tiles[idx]);
+        std::push_heap(heap.begin(), heap.end(), std::greater<std::pair<double, int>>());
+      }
+    }
+    size_t maxlen = 0;
+    for (const auto& l : lists) maxlen = std::max(maxlen, l.size());
+    plan->tiles.assign((maxlen + 1) * G, TileDesc{-1, 0, 0, 0, 0, 0, -1, -1});
+    for (int w = 0; w < G; ++w)
+      for (size_t k = 0; k < lists[w].size(); ++k) plan->tiles[k * G + w] = all_tiles[lists[w][k]];
+    plan->launch_grid = T > 0 ? G : 0;
+  }
   return MXMOE_GG_OK;
 }
 
@@ -826,7 +880,9 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
   info->variant = variant;
   info->problem_count = (int)plan.meta.size();
   info->total_tiles = plan.total_tiles;
-  info->grid = (int)plan.tiles.size();
+  info->grid = plan.launch_grid;
+  info->tile_slots = (int)plan.tiles.size();
+  info->reserved = 0;
   info->block = v.threads;
   info->lds_bytes = v.lds_bytes;
   info->qtype_mask = 0;
@@ -984,7 +1040,7 @@ int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const m
   if (plan_signature(plan) != info->signature || (int)plan.meta.size() != info->problem_count)
     return fail(MXMOE_GG_ERR_INVALID, "mxmoe_gg_rebind: problems differ from the planned call (shapes, quant "
                                       "params or strides); plan again");
-  const WsLayout l = ws_layout(info->problem_count, info->grid, info->splitk_slabs);
+  const WsLayout l = ws_layout(info->problem_count, info->tile_slots, info->splitk_slabs);
   std::vector<uint8_t> cols(5 * l.ptr, 0);
   for (int c = 0; c < 5; ++c)
     for (size_t i = 0; i < plan.order.size(); ++i) {
@@ -1004,7 +1060,7 @@ int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream) {
   if (st) return st;
   if (info->total_tiles == 0) return MXMOE_GG_OK;
   const int P = info->problem_count;
-  const WsLayout l = ws_layout(P, info->grid, info->splitk_slabs);
+  const WsLayout l = ws_layout(P, info->tile_slots, info->splitk_slabs);
   const uint8_t* ws = static_cast<const uint8_t*>(info->workspace);
   GGArgs a;
   a.meta = reinterpret_cast<const GGMeta*>(ws);

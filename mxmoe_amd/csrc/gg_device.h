@@ -509,10 +509,10 @@ __device__ __forceinline__ void lds_barrier() {
 // acquires, re-zeroes the counter for the next launch and sums every slab in slice order.
 // Returns true when `acc` holds the complete K sum (not split, or the last slice).
 template <int NT, class Acc, int FM, int FN>
-__device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& sk, uint8_t* lds) {
+__device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& sk, uint8_t* lds,
+                                              int tid = threadIdx.x) {
   if (sk.nsplit <= 1) return true;
   static_assert(FM * FN * NT * 16 <= SPLITK_SLAB_BYTES, "tile accumulators exceed one slab");
-  const int tid = threadIdx.x;
   Acc* mine = reinterpret_cast<Acc*>(sk.slabs + (size_t)(sk.slab + sk.idx) * SPLITK_SLAB_BYTES);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -2136,6 +2136,520 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
       g_gg_trace[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
       g_gg_trace[blockIdx.x * 4 + 3] = hw;
     }
+  }
+}
+
+
+// ============================================================================================
+// v2p: the persistent v2x. One 512-thread workgroup per CU walks a planned list of tiles
+// (TileDesc table laid out [k][workgroup], k-th tile of workgroup w at k * gridDim.x + w; the list
+// ends at the first prob < 0). The tile body is v2x's mainloop (3-stage B ring, buffer-form LDS-DMA
+// spread over the MFMAs, early waves issuing their partners' pieces) with two hand-offs between
+// consecutive tiles of a workgroup instead of a kernel-level block boundary:
+//   * after tile i's last barrier every ring slot is free: tile i+1's stage 0 (A and B) and B(1)
+//     are issued into A slot 0 / B slots 0-1 BEFORE tile i's epilogue (same quant type and tile
+//     height only), so their latency hides under the epilogue;
+//   * tile i's epilogue stages C through LDS in the slots that prefetch does not touch (A slot 1
+//     for waves 0-3, B slot 2 for waves 4-7, 64 rows per pass) and issues exactly WTM / 8 buffer
+//     stores per wave (masked lanes get an out-of-range offset instead of a branch), so tile i+1's
+//     first wait can count them: vmcnt(stores + B(1) pieces) leaves the stores draining under the
+//     next tile's first MFMAs.
+// LDS map: A slots [0, 32K) [32K, 64K); B ring [64K, 96K) [96K, 128K) [128K, 160K).
+// ============================================================================================
+constexpr int P_ASLOT = 32768, P_BBASE = 65536, P_BSLOT = 32768;
+
+struct PTile {  // one planned tile with its problem resolved
+  GGMeta mt;
+  const uint8_t* A;
+  const uint8_t* B;
+  const _Float16* SA;
+  const _Float16* SB;
+  _Float16* C;
+  int m0, n0, cls;
+  SplitK sk;
+};
+
+// Resolve tile slot `idx` of the table (false: an empty slot). `a` is passed through an opaque
+// copy by the caller where a second resolve must really reload (so the compiler does not keep the
+// first resolve's ~40 scalar registers live across a mainloop instead).
+// Wave-uniform copies (v_readfirstlane): once the persistent kernel has stored C, hipcc can no
+// longer prove the plan tables unmodified and loads them with vector loads; without these the buffer
+// resources built from them land in VGPRs and every LDS-DMA becomes a waterfall loop
+// (cdna_hip_programming.md T20).
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni(int64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <class T>
+__device__ __forceinline__ T* uni(T* p) {
+  return reinterpret_cast<T*>(uni((int64_t)reinterpret_cast<uintptr_t>(p)));
+}
+
+// Scalar (SMEM) loads of the plan tables, by inline asm: hipcc turns these loads into VECTOR loads
+// once the persistent kernel has stored C (it cannot prove the tables unclobbered), and a vector load
+// waits behind every older store and LDS-DMA (in-order vmcnt) — 1.5-2 us per tile boundary. SMEM
+// loads count on lgkmcnt instead. The tables are read-only during a launch (written by the host).
+typedef int32_t v8s_t __attribute__((ext_vector_type(8)));
+typedef int32_t v16s_t __attribute__((ext_vector_type(16)));
+// (each asm statement waits for its own loads: a register an asm statement defines may be read by
+// the compiler right after it, so no load may be left in flight across statements; the outputs are
+// early-clobber because several loads share one statement)
+__device__ __forceinline__ TileDesc p_tile(const GGArgs& a, int idx) {
+  v8s_t v;
+  asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(v) : "s"(a.tiles + idx) : "memory");
+  return __builtin_bit_cast(TileDesc, v);
+}
+// problem row `prob`: its GGMeta and its five pointers, one batch of scalar loads
+__device__ __forceinline__ void p_problem(const GGArgs& a, int prob, v16s_t& meta, uint64_t& pa, uint64_t& pb,
+                                          uint64_t& psa, uint64_t& psb, uint64_t& pc) {
+  asm volatile(
+      "s_load_dwordx16 %0, %6, 0x0\n\t"
+      "s_load_dwordx2 %1, %7, 0x0\n\t"
+      "s_load_dwordx2 %2, %8, 0x0\n\t"
+      "s_load_dwordx2 %3, %9, 0x0\n\t"
+      "s_load_dwordx2 %4, %10, 0x0\n\t"
+      "s_load_dwordx2 %5, %11, 0x0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(meta), "=&s"(pa), "=&s"(pb), "=&s"(psa), "=&s"(psb), "=&s"(pc)
+      : "s"(a.meta + prob), "s"(a.ptr_A + prob), "s"(a.ptr_B + prob), "s"(a.ptr_SA + prob), "s"(a.ptr_SB + prob),
+        "s"(a.ptr_C + prob)
+      : "memory");
+}
+__device__ __forceinline__ int p_qtype(const GGArgs& a, int prob) {
+  int q;
+  asm volatile("s_load_dword %0, %1, 0xc\n\ts_waitcnt lgkmcnt(0)" : "=&s"(q) : "s"(a.meta + prob) : "memory");
+  return q;
+}
+
+__device__ __forceinline__ bool p_resolve(const GGArgs& a, int idx, PTile& pt) {
+  const TileDesc td = p_tile(a, idx);
+  const int prob = uni(td.prob);
+  if (prob < 0) return false;
+  v16s_t mv;
+  uint64_t pa, pb, psa, psb, pc;
+  p_problem(a, prob, mv, pa, pb, psa, psb, pc);
+  const GGMeta m = __builtin_bit_cast(GGMeta, mv);
+  pt.mt.M = uni(m.M);
+  pt.mt.N = uni(m.N);
+  pt.mt.K = uni(m.K);
+  pt.mt.qtype = uni(m.qtype);
+  pt.mt.tiles_n = uni(m.tiles_n);
+  pt.mt.tile_begin = uni(m.tile_begin);
+  pt.mt.kbytes = uni(m.kbytes);
+  pt.mt.reserved = uni(m.reserved);
+  pt.mt.lda_b = uni(m.lda_b);
+  pt.mt.ldb_b = uni(m.ldb_b);
+  pt.mt.ldc = uni(m.ldc);
+  pt.mt.reserved2 = uni(m.reserved2);
+  pt.A = reinterpret_cast<const uint8_t*>(pa);
+  pt.B = reinterpret_cast<const uint8_t*>(pb);
+  pt.SA = reinterpret_cast<const _Float16*>(psa);
+  pt.SB = reinterpret_cast<const _Float16*>(psb);
+  pt.C = reinterpret_cast<_Float16*>(pc);
+  pt.m0 = uni(td.m0);
+  pt.n0 = uni(td.n0);
+  const int cls = uni(td.cls);
+  pt.cls = cls & 0xFF;
+  pt.sk.ks0 = uni(td.ks0);
+  pt.sk.nst = uni(td.ks1) - pt.sk.ks0;
+  pt.sk.idx = (cls >> 8) & 0xFF;
+  pt.sk.nsplit = (cls >> 16) & 0xFF;
+  pt.sk.slab = uni(td.slab);
+  pt.sk.grp = uni(td.grp);
+  pt.sk.slabs = a.slabs;
+  pt.sk.counters = a.counters;
+  return true;
+}
+
+__device__ __forceinline__ GGArgs p_opaque(const GGArgs& a) {
+  GGArgs o = a;
+  asm volatile("" : "+s"(o.tiles), "+s"(o.meta), "+s"(o.ptr_A), "+s"(o.ptr_B));
+  asm volatile("" : "+s"(o.ptr_SA), "+s"(o.ptr_SB), "+s"(o.ptr_C));
+  return o;
+}
+
+struct PTileResult {
+  bool pref;   // the next tile's first stages were issued
+  int stores;  // buffer stores this wave issued in the epilogue (all after the prefetch)
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {  // runtime count, bounded by N (unrolled compare chain)
+  if constexpr (N > 0) {
+    if (n >= N) {
+      wait_vmcnt<N>();
+      return;
+    }
+    wait_vmcnt_rt<N - 1>(n);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
+template <class Cfg, int QT, int TRACE = 0>
+__device__ __forceinline__ PTileResult gg_tile_v2p(const GGArgs& args, int cur_idx, int nx_idx, bool prefetched,
+                                                   int s_prev, uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
+  typedef typename AccT<QT>::type acc_t;
+  typedef V2Half<Cfg, QT, 0> Half;
+  constexpr bool EDMA = QT != QT_I4;  // int4 half stages carry twice the MFMAs: no slack in the early waves
+  constexpr int HALFW = Cfg::WM * Cfg::WN / 2;
+  constexpr int NH = Half::kMfma, NR = Half::kReads, ND = GA + GB;
+  constexpr int NDE = EDMA ? 2 * ND : ND;
+  constexpr int KSE = 4 * NDE <= NH ? 4 : (NH / NDE > 0 ? NH / NDE : 1);
+  constexpr int RESTE = NH - KSE * NDE > 0 ? NH - KSE * NDE : 0;
+  constexpr int SPW = Cfg::WTM / 8;  // epilogue buffer stores per wave
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // per tile: nothing lane-derived is hoisted out of the persistent loop
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const bool early = wave < HALFW;
+  const int pw = EDMA ? (early ? 2 : 0) : 1;  // LDS-DMA pieces this wave issues per (operand, row group)
+  PTile t;
+  p_resolve(args, cur_idx, t);
+  const GGMeta& mt = t.mt;
+  const int kbytes = mt.kbytes;
+  const int nst = t.sk.nst, ks0 = t.sk.ks0;
+  const int M = mt.M, N = mt.N;
+
+  auto abuf = [&](int s) { return lds + (s & 1) * P_ASLOT; };
+  auto bbuf = [&](int s) { return lds + P_BBASE + (s % 3) * P_BSLOT; };
+  // buffer resources of a tile (rows past M / N read as zeros) and its fixed lane offsets
+  auto rsrc = [&](const uint8_t* base, int64_t ld, int rows) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, (int)(rows * ld), 0x00020000);
+  };
+  auto lane_off = [&](int G, int j, int64_t ld) {
+    const int row = (wave * G + j) * 8 + (lane >> 3);
+    return (uint32_t)(row * ld) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
+  };
+  // the pieces of one operand of stage kb (bytes) into dst: this wave's rows, and (EDMA, early
+  // waves) its partner's rows (8 * G * HALFW further, the same swizzle)
+  auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, const uint32_t* vo, int G, int64_t ld, int kb, int kbytes_,
+                 bool full, uint8_t* dst) {
+    if (EDMA && !early) return;
+    const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+    for (int w2 = 0; w2 < (EDMA ? 2 : 1); ++w2) {
+      const int ww = wave + w2 * HALFW;
+      const uint32_t radd = (uint32_t)(w2 * 8 * G * HALFW * ld);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= G) break;
+        const int kc = (p ^ ((((wave * G + j) * 8 + rsub) >> 1) & 7)) << 4;
+        const bool in = full || kb + kc < kbytes_;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + (ww * G + j) * 1024), 16,
+                                                 in ? vo[j] + radd : 0x80000000u, kb, 0, 0);
+      }
+    }
+  };
+
+  const __amdgpu_buffer_rsrc_t rsA = rsrc(t.A + (int64_t)t.m0 * mt.lda_b, mt.lda_b, min(M - t.m0, Cfg::BM));
+  const __amdgpu_buffer_rsrc_t rsB = rsrc(t.B + (int64_t)t.n0 * mt.ldb_b, mt.ldb_b, min(N - t.n0, Cfg::BN));
+  uint32_t voA[4], voB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    voA[j] = j < GA ? lane_off(GA, j, mt.lda_b) : 0u;
+    voB[j] = j < GB ? lane_off(GB, j, mt.ldb_b) : 0u;
+  }
+  const int nst_full = (ks0 + nst) * Cfg::BKB > kbytes ? nst - 1 : nst;
+  auto full_stage = [&](int s) { return s < nst_full; };
+  auto dma_a = [&](int s, bool full) { dma(rsA, voA, GA, mt.lda_b, (ks0 + s) * Cfg::BKB, kbytes, full, abuf(s)); };
+  auto dma_b = [&](int s, bool full) { dma(rsB, voB, GB, mt.ldb_b, (ks0 + s) * Cfg::BKB, kbytes, full, bbuf(s)); };
+  auto dma_steady = [&](int s) {
+    dma_a(s + 1, true);
+    dma_b(s + 2, true);
+  };
+  auto dma_generic = [&](int s) {
+    if (s + 1 < nst) dma_a(s + 1, full_stage(s + 1));
+    if (s + 2 < nst) dma_b(s + 2, full_stage(s + 2));
+  };
+  const int nsteady = nst_full - 2;
+  auto stage_wait = [&](int s) {
+    if (s + 2 < nst) wait_vmcnt<(EDMA ? 2 : 1) * GB>();
+    else wait_vmcnt<0>();
+  };
+  const int swz = (r16 >> 1) & 7;
+  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
+  const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
+  auto hread = [&](Half& f, int s, int h) { f.read(abuf(s), bbuf(s), a_row, b_row, swz, g, h); };
+  acc_t acc[FM][FN];
+  auto hmma = [&](const Half& f) { f.mma(acc); };
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+
+  // (TRACE, lab diagnostics: per tile slot {start, mainloop end, epilogue issued, info} in g_gg_trace)
+  [[maybe_unused]] auto tmark = [&](int slot) {
+    if constexpr (TRACE != 0) {
+      if (tid == 0 && cur_idx < kTraceBlocks) g_gg_trace[cur_idx * 4 + slot] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  tmark(0);
+  // ---- prologue: stage 0 + B(1) (issued by the previous tile when prefetched) ----
+  if (nst > 0) {
+    if (!prefetched) {
+      dma_a(0, full_stage(0));
+      dma_b(0, full_stage(0));
+      if (nst > 1) dma_b(1, full_stage(1));
+      stage_wait(-1);
+    } else {
+      // outstanding, oldest first: [A(0), B(0), B(1)] (prefetch) then the previous epilogue's
+      // s_prev stores; A(0) and B(0) must have landed
+      wait_vmcnt_rt<3 * 16>(s_prev + (nst > 1 ? pw * GB : 0));
+    }
+    lds_barrier();
+    Half fr;
+    if (!early) {  // late waves
+      dma_generic(0);
+      hread(fr, 0, 0);
+      hmma(fr);
+      hread(fr, 0, 1);
+      stage_wait(0);
+      lds_barrier();
+      int s = 1;
+      for (; s < nsteady; ++s) {
+        dma_steady(s);
+        hmma(fr);
+        hread(fr, s, 0);
+        hmma(fr);
+        hread(fr, s, 1);
+        if constexpr (EDMA) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        } else {
+#pragma unroll
+          for (int q = 0; q < ND; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, KSE, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, RESTE, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        }
+        stage_wait(s);
+        lds_barrier();
+      }
+      for (; s < nst; ++s) {
+        dma_generic(s);
+        hmma(fr);
+        hread(fr, s, 0);
+        hmma(fr);
+        hread(fr, s, 1);
+        stage_wait(s);
+        lds_barrier();
+      }
+      hmma(fr);
+    } else {  // early waves
+      int s = 0;
+      for (; s < nsteady; ++s) {
+        hread(fr, s, 0);
+        dma_steady(s);
+        hmma(fr);
+        hread(fr, s, 1);
+        hmma(fr);
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+        for (int q = 0; q < NDE; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, KSE, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, RESTE, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
+        stage_wait(s);
+        lds_barrier();
+      }
+      for (; s < nst; ++s) {
+        dma_generic(s);
+        hread(fr, s, 0);
+        hmma(fr);
+        hread(fr, s, 1);
+        hmma(fr);
+        stage_wait(s);
+        lds_barrier();
+      }
+    }
+  } else {
+    __syncthreads();
+  }
+
+  tmark(1);
+  // ---- between the tiles: scales (int paths) into registers, then the next tile's first stages ----
+  // (both tiles re-resolved from memory: nothing of the mainloop's setup stays live across it)
+  int ci = __builtin_amdgcn_readfirstlane(cur_idx), ni = __builtin_amdgcn_readfirstlane(nx_idx);
+  asm volatile("" : "+s"(ci), "+s"(ni));  // opaque indices: the resolves below reload (scalar loads)
+  PTile nx;
+  p_resolve(args, ci, t);
+  const bool nx_ok = ni >= 0 && p_resolve(args, ni, nx) && nx.mt.qtype == QT && nx.cls == t.cls;
+  int etid = tid;
+  asm volatile("" : "+v"(etid));  // keep the lane decomposition out of the mainloop's live set
+  const int e_lane = etid & 63, e_r16 = e_lane & 15, e_g = e_lane >> 4;
+  const int mrow0 = t.m0 + wm * Cfg::WTM, ncol0 = t.n0 + wn * Cfg::WTN;
+  const int Me = t.mt.M, Ne = t.mt.N;
+  [[maybe_unused]] _Float16 sai[FM];
+  [[maybe_unused]] uint2 sbw[FN];
+  if constexpr (qt_scaled(QT)) {  // (global, not flat, loads: a flat load would make hipcc wait vmcnt(0))
+    typedef const __attribute__((address_space(1))) _Float16 gh_t;
+    typedef const __attribute__((address_space(1))) uint64_t gu64_t;
+    gh_t* sa = (gh_t*)(t.SA);
+    gh_t* sb = (gh_t*)(t.SB);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) sai[i] = sa[min(mrow0 + i * 16 + e_r16, Me - 1)];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = min(ncol0 + j * 16 + 4 * e_g, Ne - 4);  // N % 8 == 0: a 4-column group stays in range
+      sbw[j] = __builtin_bit_cast(uint2, *(gu64_t*)(sb + c));
+    }
+  }
+  const bool narrow = (int64_t)Cfg::WTM * t.mt.ldc < (int64_t)1 << 29;  // C byte offsets < 2^30
+  const bool split = t.sk.nsplit > 1;
+#ifdef V2P_NO_PREF
+  const bool pref = false && nx_ok;
+#else
+  const bool pref = nx_ok && narrow && !split && nst > 0;
+#endif
+  int npref = 0;
+  if (pref) {
+    const GGMeta& nm = nx.mt;
+    const __amdgpu_buffer_rsrc_t nA = rsrc(nx.A + (int64_t)nx.m0 * nm.lda_b, nm.lda_b, min(nm.M - nx.m0, Cfg::BM));
+    const __amdgpu_buffer_rsrc_t nB = rsrc(nx.B + (int64_t)nx.n0 * nm.ldb_b, nm.ldb_b, min(nm.N - nx.n0, Cfg::BN));
+    uint32_t vA[4], vB[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vA[j] = j < GA ? lane_off(GA, j, nm.lda_b) : 0u;
+      vB[j] = j < GB ? lane_off(GB, j, nm.ldb_b) : 0u;
+    }
+    const int nks0 = nx.sk.ks0, nnst = nx.sk.nst;
+    const int nfull = (nks0 + nnst) * Cfg::BKB > nm.kbytes ? nnst - 1 : nnst;
+    if (nnst > 0) {
+      dma(nA, vA, GA, nm.lda_b, nks0 * Cfg::BKB, nm.kbytes, 0 < nfull, abuf(0));
+      dma(nB, vB, GB, nm.ldb_b, nks0 * Cfg::BKB, nm.kbytes, 0 < nfull, bbuf(0));
+      npref = pw * (GA + GB);
+      if (nnst > 1) {
+        dma(nB, vB, GB, nm.ldb_b, (nks0 + 1) * Cfg::BKB, nm.kbytes, 1 < nfull, bbuf(1));
+        npref += pw * GB;
+      }
+    }
+  }
+  if constexpr (qt_scaled(QT)) wait_vmcnt_rt<3 * 16>(npref);  // the scale loads (older than the prefetch)
+  if (split && !splitk_reduce<Cfg::NT>(acc, t.sk, lds)) return PTileResult{false, 0};
+
+  // ---- epilogue: per-wave staging in the slots the prefetch leaves alone, 64 rows per pass ----
+  constexpr int RP = Cfg::WTM < 64 ? Cfg::WTM : 64;
+  uint8_t* reg = early ? lds + P_ASLOT + wave * 8192 : lds + P_BBASE + 2 * P_BSLOT + (wave - HALFW) * 8192;
+  const int64_t ldc = t.mt.ldc;
+  _Float16* const cbase = t.C + (int64_t)mrow0 * ldc + ncol0;  // wave-uniform
+  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int pass = 0; pass < Cfg::WTM / RP; ++pass) {
+#pragma unroll
+    for (int i = pass * RP / 16; i < (pass + 1) * RP / 16; ++i) {
+      const int ml = i * 16 + e_r16 - pass * RP;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        uint2 pk;
+        if constexpr (QT == QT_F16 || QT == QT_BF16) pk = pack4_f16(acc[i][j]);
+        else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai[i], sbw[j]);
+        const int q = 2 * j + (e_g >> 1);
+        *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
+      }
+    }
+    // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
+#pragma unroll
+    for (int it = 0; it < RP / 8; ++it) {
+      const int rl = it * 8 + (e_lane >> 3), q = e_lane & 7;
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + rl * 128 + ((q ^ (rl & 7)) << 4));
+      const int row = pass * RP + rl;
+      const int m = mrow0 + row, n = ncol0 + q * 8;
+      if (narrow) {
+        typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+        const v4u_ d = {v.x, v.y, v.z, v.w};
+        const uint32_t off = (m < Me && n < Ne) ? (uint32_t)(((int64_t)row * ldc + q * 8) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(d, rsC, (int)off, 0, 16 /* sc1 */);
+      } else if (m < Me && n < Ne) {
+        *reinterpret_cast<uint4*>(cbase + (int64_t)row * ldc + q * 8) = v;
+      }
+    }
+  }
+  if constexpr (TRACE != 0) {
+    if (tid == 0 && cur_idx < kTraceBlocks) {
+      g_gg_trace[cur_idx * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+      g_gg_trace[cur_idx * 4 + 3] = ((uint64_t)(__builtin_amdgcn_s_getreg((19 << 11) | 20) & 0xF) << 32) |
+                                    ((uint64_t)(QT & 0xF) << 36) | ((uint64_t)(t.cls & 0xFF) << 40) |
+                                    ((uint64_t)(nst & 0xFFFF) << 48) | (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
+  }
+  return PTileResult{pref, pref ? SPW : 0};
+}
+
+template <int QM, int TRACE = 0>
+__global__ __launch_bounds__(512, 2) void gg_v2p_kernel(GGArgs args) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[160 * 1024];
+  const int G = gridDim.x;
+  auto family = [](int qt) { return qt == QT_F16 || qt == QT_I8 || qt == QT_I4 || qt == QT_BF16; };
+  bool pref = false;
+  int s_prev = 0;
+  for (int k = 0;; ++k) {
+    const int idx = k * G + blockIdx.x;
+    const TileDesc td = p_tile(args, idx);
+    const int prob = uni(td.prob);
+    if (prob < 0) break;
+    const int nx_idx = uni(p_tile(args, idx + G).prob) >= 0 ? idx + G : -1;
+    const int qt = uni(p_qtype(args, prob)), cls = uni(td.cls) & 0xFF;
+    if (!pref && k > 0) __syncthreads();  // the previous tile's LDS use is over for every wave
+    PTileResult r{false, 0};
+    bool done = false;
+#define MXMOE_V2P(Q, BMC)                                                                              \
+  if (!done && (QM & (1 << Q)) && qt == Q && cls == BMC) {                                             \
+    r = gg_tile_v2p<V2Cfg<(BMC) == 0 ? 256 : (BMC) == 1 ? 128 : 64>, Q, TRACE>(args, idx, nx_idx, pref, s_prev, lds); \
+    done = true;                                                                                       \
+  }
+    MXMOE_V2P(QT_I8, 0)
+    MXMOE_V2P(QT_I8, 1)
+    MXMOE_V2P(QT_I4, 0)
+    MXMOE_V2P(QT_I4, 1)
+    MXMOE_V2P(QT_F16, 0)
+    MXMOE_V2P(QT_F16, 1)
+    MXMOE_V2P(QT_F16, 2)
+    MXMOE_V2P(QT_BF16, 0)
+    MXMOE_V2P(QT_BF16, 1)
+    MXMOE_V2P(QT_BF16, 2)
+#undef MXMOE_V2P
+    if (!done && !family(qt)) {  // the other tile bodies (their own prologue / LDS use; never prefetched into)
+      PTile cur;
+      p_resolve(args, idx, cur);
+      const SplitK& sk = cur.sk;
+      if ((QM & (1 << QT_I4G)) && qt == QT_I4G) {
+        if (cls == 0) gg_tile_g128<V2Cfg<256>>(cur.mt, cur.A, cur.B, cur.SA, cur.SB, cur.C, cur.m0, cur.n0, lds);
+        else gg_tile_g128<V2Cfg<128>>(cur.mt, cur.A, cur.B, cur.SA, cur.SB, cur.C, cur.m0, cur.n0, lds);
+      } else if ((QM & (1 << QT_F8)) && qt == QT_F8) {
+        if (cls == 0) gg_tile_v2<V2Cfg<256>, QT_F8, 0>(cur.mt, cur.A, cur.B, cur.SA, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else gg_tile_v2<V2Cfg<128>, QT_F8, 0>(cur.mt, cur.A, cur.B, cur.SA, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+      } else if ((QM & (1 << QT_W4A16)) && qt == QT_W4A16) {
+        if (cls == 0) gg_tile_wo<WoCfg<256>, 4>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else gg_tile_wo<WoCfg<64, 1>, 4>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+      } else if ((QM & (1 << QT_W8A16)) && qt == QT_W8A16) {
+        if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else gg_tile_wo<WoCfg<64, 1>, 8>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+      } else if ((QM & (1 << QT_W2A16)) && qt == QT_W2A16) {
+        if (cls == 0) gg_tile_wo<WoCfg<256>, 2>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 2>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+        else gg_tile_wo<WoCfg<64, 1>, 2>(cur.mt, cur.A, cur.B, cur.SB, cur.C, cur.m0, cur.n0, lds, sk);
+      }
+      __syncthreads();  // the body's LDS use ends for every wave before the next tile's DMA
+    }
+    pref = r.pref;
+    s_prev = r.stores;
   }
 }
 

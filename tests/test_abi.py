@@ -61,7 +61,7 @@ def test_workspace_size_grows_with_tiles():
 
 
 def test_struct_plan_info_layout():
-    assert ctypes.sizeof(nat.GGPlanInfo) == 8 * 4 + 8 + 8 + 8  # + the plan signature
+    assert ctypes.sizeof(nat.GGPlanInfo) == 8 * 4 + 8 + 8 + 8 + 8  # + the plan signature, tile_slots
 
 
 def test_auto_variant_follows_quant_mix():

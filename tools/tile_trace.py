@@ -109,7 +109,7 @@ def main():
     fetch(0, reset=True)
     gg.launch()
     torch.cuda.synchronize()
-    tr = fetch(gg.info.grid, reset=False)
+    tr = fetch(max(gg.info.grid, gg.info.tile_slots), reset=False)
     res = {"variant": args.variant_name, "cfg": args.cfg, "gg": args.dense or args.gg, "bs": args.bs, "env": args.env, "event_median_ms": round(t["median_ms"], 4)}
     res.update(analyse(tr))
     print(json.dumps(res), flush=True)
