@@ -479,6 +479,7 @@ struct Plan {
   int total_tiles = 0;
   int launch_grid = 0;          // workgroups launched (= tiles.size() unless persistent)
   int slabs = 0;                // split-K partial slabs
+  int tail_slabs = 0;           // of which for the tail split (plan_host)
 };
 
 // Tile generation + scheduling.
@@ -589,6 +590,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   plan->meta.clear();
   plan->order = order;
   plan->slabs = 0;
+  plan->tail_slabs = 0;
   const int chunk = v.chunk;
   // XCD regions. Within one XCD, consecutive tiles run together (the XCD hands each freed CU its
   // next block), so a band's A rows and B columns are re-read from that XCD's L2 while they are
@@ -770,6 +772,87 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     s0 = s1;
   }
   if (regions_last) put_regions();
+
+#ifdef MXMOE_LAB
+  // Tail split (v2, not persistent). An XCD hands its blocks to its CUs in queue order, so the
+  // queue's last tiles run while most of the XCD's CUs have gone idle for good (w8a8 down at
+  // bs=8192: 194 tiles per XCD = 6 rounds of 32 + 2; tile timelines put the ragged finish at
+  // 6-8 % of CU time). Per XCD, the tiles that start after the first CU's last tile ended are cut
+  // along K into S consecutive slices (the split-K path above), S in 2..8 (>= 3 stages a slice,
+  // each slice priced at 2 extra stages for its fill and partial-sum traffic) chosen to minimise
+  // the XCD's simulated finish; kept only if that gains >= 1 %.
+  // MEASURED NEGATIVE: 1.5-2 % slower on the w8a8 / fp16 / mixed gate_up calls, the
+  // only layer-11 calls it cuts (the partial-sum round trip costs more than the ragged finish
+  // it removes). Lab library only, opt-in: MXMOE_GG_TAIL_SPLIT=1.
+  const char* ts_env = planner_knob("MXMOE_GG_TAIL_SPLIT");
+  if (v.kind == Kind::V2 && !v.persistent && ts_env && ts_env[0] == '1') {
+    auto simulate = [&](const std::vector<double>& t, std::vector<double>* starts) {
+      std::vector<double> slot(chunk, 0.0);  // min-heap of slot free times
+      double finish = 0;
+      for (size_t j = 0; j < t.size(); ++j) {
+        std::pop_heap(slot.begin(), slot.end(), std::greater<double>());
+        if (starts) (*starts)[j] = slot.back();
+        slot.back() += t[j];
+        finish = std::max(finish, slot.back());
+        std::push_heap(slot.begin(), slot.end(), std::greater<double>());
+      }
+      return std::make_pair(finish, *std::min_element(slot.begin(), slot.end()));
+    };
+    for (int x = 0; x < 8; ++x) {
+      std::vector<int>& q = queue[x];
+      const size_t n = q.size();
+      if (n <= (size_t)chunk) continue;  // one round: nothing runs after a CU went idle
+      std::vector<double> t(n), st(n);
+      for (size_t j = 0; j < n; ++j) t[j] = tile_time(all_tiles[q[j]]);
+      const auto base = simulate(t, &st);
+      size_t j0 = n;
+      while (j0 > 0 && st[j0 - 1] >= base.second) --j0;  // starts are non-decreasing in queue order
+      auto splittable = [&](const TileDesc& td) {
+        const int qt = plan->meta[td.prob].qtype;
+        return ((td.cls >> 16) & 0xFF) <= 1 && !is_weightonly(qt) && qt != QT_I4G && td.ks1 - td.ks0 >= 6;
+      };
+      int best_s = 1;
+      double best_finish = base.first;
+      for (int S = 2; S <= 8; ++S) {
+        std::vector<double> t2(t.begin(), t.begin() + j0);
+        for (size_t j = j0; j < n; ++j) {
+          const TileDesc& td = all_tiles[q[j]];
+          const int nst = td.ks1 - td.ks0;
+          if (!splittable(td) || nst / S < 3) {
+            t2.push_back(t[j]);
+            continue;
+          }
+          const double per_stage = t[j] / nst;
+          for (int k = 0; k < S; ++k) t2.push_back(per_stage * ((k + 1) * nst / S - k * nst / S + 2));
+        }
+        const double f = simulate(t2, nullptr).first;
+        if (f < best_finish) {
+          best_finish = f;
+          best_s = S;
+        }
+      }
+      if (best_s == 1 || best_finish > 0.99 * base.first) continue;
+      std::vector<int> q2(q.begin(), q.begin() + j0);
+      for (size_t j = j0; j < n; ++j) {
+        const TileDesc td = all_tiles[q[j]];
+        const int nst = td.ks1 - td.ks0, S = best_s;
+        if (!splittable(td) || nst / S < 3) {
+          q2.push_back(q[j]);
+          continue;
+        }
+        const int grp = groups++, slab = plan->slabs;
+        plan->slabs += S;
+        plan->tail_slabs += S;
+        for (int k = 0; k < S; ++k) {
+          q2.push_back((int)all_tiles.size());
+          all_tiles.push_back(TileDesc{td.prob, td.m0, td.n0, (td.cls & 0xFF) | (k << 8) | (S << 16),
+                                       td.ks0 + k * nst / S, td.ks0 + (k + 1) * nst / S, slab, grp});
+        }
+      }
+      q.swap(q2);
+    }
+  }
+#endif
   size_t qmax = 0;
   for (const auto& q : queue) qmax = std::max(qmax, q.size());
   int grid = 0;
@@ -781,7 +864,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       grid = std::max(grid, b + 1);
     }
   plan->tiles.resize(grid);
-  plan->total_tiles = T;
+  plan->total_tiles = 0;
+  for (const auto& q : queue) plan->total_tiles += (int)q.size();
   plan->launch_grid = grid;
   if (v.persistent) {
     // v2p: each XCD's queue handed out to its `chunk` workgroups in queue order, every tile to the
@@ -834,7 +918,7 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     // int4-only: the 256x128 2-WG/CU kernel, unless the call is low-fill enough for the v2s plan
     // to split K (that kernel cannot)
     Plan p;
-    if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == 0) *out = variant_index(kInt4Variant);
+    if (plan_host(hp, *out, false, &p) == MXMOE_GG_OK && p.slabs == p.tail_slabs) *out = variant_index(kInt4Variant);
   }
   return MXMOE_GG_OK;
 }

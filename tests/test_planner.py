@@ -108,14 +108,14 @@ def test_shared_expert_one_rectangle_per_xcd():
     q = _xcd_queues(tiles)
     for x in range(8):
         is_shared = [int(rows[t[0]]) == shared for t in q[x]]
-        n = sum(is_shared)
-        assert n == 32 * 44 // 8
+        n = sum(is_shared)  # queue entries (a tail-split tile is several)
+        st = np.array([t for t, s in zip(q[x], is_shared) if s])
+        assert len({(int(t[1]), int(t[2])) for t in st}) == 32 * 44 // 8
         # the region closes the XCD's queue
         assert all(is_shared[-n:]) and not any(is_shared[:-n]), "region tiles must close the XCD queue"
-        st = np.array([t for t, s in zip(q[x], is_shared) if s])
         m_panels, n_panels = len(np.unique(st[:, 1])), len(np.unique(st[:, 2]))
         # a rectangle: every (m, n) pair of its rows x columns
-        assert m_panels * n_panels == n
+        assert m_panels * n_panels == 32 * 44 // 8
         assert m_panels + n_panels <= 48  # 4 x 44 (vs 32 + 44 for a region of whole rows)
 
 
