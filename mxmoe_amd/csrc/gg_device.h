@@ -589,7 +589,11 @@ enum : int {
   V2_PRIO_LATE = 1 << 26,
   // weight-only timing ablations (w4a16 tiles only; WRONG RESULTS by design): B read from 8-KiB
   // stage blocks / no LDS-DMA after the ring's first fill / no fragment reads, dequant or MFMA
-  ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14
+  ABL_WO_BTILED = 1 << 14, ABL_WO_NODMA = 2 << 14, ABL_WO_NOCOMPUTE = 4 << 14,
+  // weight-only option (correct results): the 128 / 64-row tiles read stage s+1's fragments into a
+  // second register set right after the barrier that publishes it, and run stage s's dequant +
+  // MFMAs while those reads are in flight (gg_tile_wo)
+  WO_PIPE = 1 << 17
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -2029,7 +2033,107 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     if constexpr (DIST >= 2) if (later == 1) { wait_vmcnt<DPS>(); return; }
     wait_vmcnt<0>();
   };
-  if (nst > 0) {
+  // WO_PIPE (128 / 64-row tiles, WM = 1: their fragment sets are small): the fragments of stage
+  // s+1 are read into a second register set right after the barrier that publishes stage s+1,
+  // and stage s's dequant + MFMAs (first set) run while those reads are in flight; the reads no
+  // longer sit between the barrier and the MFMAs of the same stage.
+  constexpr bool PIPE = (WABL & WO_PIPE) != 0 && Cfg::WM == 1 && DIST >= 2;
+  struct Frag {
+    v8h a[2][FM];
+    uint32_t rb[FN][2][2];  // B words: [j][kc][.] (4-bit: both K halves in [j][0]; 2-bit: [j][0][0])
+  };
+  auto read_frag = [&](int buf, Frag& f) {
+    const uint8_t* As = lds + buf * SB_ + a_row;
+    const uint8_t* Bs = lds + buf * SB_ + Cfg::A_BYTES + b_row;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (BITS == 2) {
+        f.rb[j][0][0] = *reinterpret_cast<const uint32_t*>(Bs + j * 16 * RB + g * 4);
+      } else if constexpr (BITS == 4) {
+        const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + (((g >> 1) ^ bsw) << 4) + (g & 1) * 8);
+        f.rb[j][0][0] = v.x;
+        f.rb[j][0][1] = v.y;
+      } else {
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+          const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + ((g ^ bsw) << 4) + kc * 8);
+          f.rb[j][kc][0] = v.x;
+          f.rb[j][kc][1] = v.y;
+        }
+      }
+    }
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const uint32_t off = (uint32_t)(((kc * 4 + g) ^ swz) << 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) f.a[kc][i] = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
+    }
+  };
+  auto mma_frag = [&](const Frag& f) {
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      v8h b[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (BITS == 2) {
+          const uint32_t w = f.rb[j][0][0] >> (8 * kc);
+          b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j]);
+        } else if constexpr (BITS == 4) {
+          b[j] = wo_dequant<4>(&f.rb[j][0][kc], moff2, s2[j], z2[j]);
+        } else {
+          b[j] = wo_dequant<8>(f.rb[j][kc], moff2, s2[j], z2[j]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], f.a[kc][i], acc[i][j], 0, 0, 0);
+    }
+  };
+  if constexpr (PIPE) {
+   if (nst > 0) {
+    load_scales(ks0 / gstages, s2, z2);
+#pragma unroll
+    for (int p = 0; p < DIST; ++p)
+      if (p < nst) issue(p, p);
+    if (DIST - 1 < nst) wait_vmcnt<(DIST - 1) * DPS>();
+    else wait_stage(nst - 1);
+    lds_barrier();  // stage 0 visible
+    Frag fa, fb;
+    read_frag(0, fa);
+    int gpos = (ks0 + 1) % gstages;
+    // iteration s: publish stage s+1 (wait + barrier; every wave's reads of stage s are done, so
+    // the buffer of stage s-1 is free for stage s+DIST), issue it, read it into the other set,
+    // then stage s's dequant + MFMAs
+    auto step = [&](int s, Frag& cur, Frag& nxt) {
+      if (s + 1 < nst) {
+        // stages issued after s+1: min(DIST - 2, nst - 2 - s)
+        if (s + DIST < nst) wait_vmcnt<(DIST - 2) * DPS>();
+        else wait_stage(nst - 2 - s);
+        lds_barrier();
+      }
+      const bool next_group = gpos == 0 && s + 1 < nst;
+      gpos = gpos + 1 == gstages ? 0 : gpos + 1;
+      if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);
+      if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
+      if (s + 1 < nst) read_frag((s + 1) % NBUF, nxt);
+      mma_frag(cur);
+      if (next_group) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          s2[j] = s2n[j];
+          z2[j] = z2n[j];
+        }
+      }
+    };
+    for (int s = 0; s < nst; s += 2) {
+      step(s, fa, fb);
+      if (s + 1 < nst) step(s + 1, fb, fa);
+    }
+    wait_vmcnt<0>();
+    lds_barrier();  // ring -> epilogue staging
+   }
+  } else if (nst > 0) {
     load_scales(ks0 / gstages, s2, z2);
 #pragma unroll
     for (int p = 0; p < DIST; ++p)
@@ -2114,18 +2218,20 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
     else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v2<V2Cfg<64>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
-    constexpr int WABL = ABL & kWoAblMask;
+    constexpr int WABL = ABL & (kWoAblMask | WO_PIPE);
     if (cls == 0) gg_tile_wo<WoCfg<256>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_wo<WoCfg<64, 1>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
-    if (cls == 0) gg_tile_wo<WoCfg<256>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    else gg_tile_wo<WoCfg<64, 1>, 8>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    constexpr int WP = ABL & WO_PIPE;
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_wo<WoCfg<64, 1>, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) {
-    if (cls == 0) gg_tile_wo<WoCfg<256>, 2>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 2>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    else gg_tile_wo<WoCfg<64, 1>, 2>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    constexpr int WP = ABL & WO_PIPE;
+    if (cls == 0) gg_tile_wo<WoCfg<256>, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_wo<WoCfg<64, 1>, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   }
   if constexpr ((ABL & V2_TRACE) != 0) {
     if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) {

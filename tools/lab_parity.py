@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from mxmoe_amd import _native as nat  # noqa: E402
-from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, group_gemm  # noqa: E402
+from mxmoe_amd.groupgemm import FP16, W4A4, W8A8, QParams, group_gemm  # noqa: E402
 from tests._util import HostProblem, assert_f16_close, exact_compare  # noqa: E402
 
 
@@ -35,6 +35,15 @@ def cases():
                                 for t in range(1, 8)]
     yield "mixed", [(300, 256, 256, W8A8), (0, 256, 256, W4A4), (129, 384, 512, W4A4), (513, 256, 1280, W8A8),
                     (5, 128, 64, W4A4), (384, 512, 2048, W8A8), (512, 768, 4096, W4A4)]
+    # weight-only w4a16 (the lab build compiles the 4-bit body only): edge shapes of
+    # tests/test_weightonly_gpu.py plus small-batch expert shapes (long K, many scale groups)
+    for g in (-1, 128):
+        for sym in (True, False):
+            q = QParams(16, 4, g, sym)
+            yield f"w4a16_g{g}_{'sym' if sym else 'asym'}", [
+                (M, N, K, q) for M, N, K in [(1, 128, 256), (17, 256, 128 if g == -1 else 256), (130, 136, 384),
+                                             (257, 264, 512), (513, 512, 1408), (64, 8, 1024), (34, 2816, 2048),
+                                             (41, 2048, 1408), (96, 512, 640)]]
 
 
 def main():
