@@ -289,6 +289,7 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | ABL_WO_NOCOMPUTE>("abl_v2s_wo_nocompute"),
       // weight-only experiment (correct results): v2x + the pipelined 128 / 64-row weight-only loop
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT) | WO_PIPE>("x_v2x_wopipe"),
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT) | WO_PIPE | WO_STAG>("x_v2x_wopipe_stag"),
 #endif
   };
   return v;

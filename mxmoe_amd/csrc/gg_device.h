@@ -593,7 +593,11 @@ enum : int {
   // weight-only option (correct results): the 128 / 64-row tiles read stage s+1's fragments into a
   // second register set right after the barrier that publishes it, and run stage s's dequant +
   // MFMAs while those reads are in flight (gg_tile_wo)
-  WO_PIPE = 1 << 17
+  WO_PIPE = 1 << 17,
+  // with WO_PIPE: waves 4-7 defer each stage's second-K-half MFMAs (operands dequantised before
+  // the barrier, held in registers) past the next barrier, so SIMD partners are half a stage
+  // apart — one wave's MFMAs beside the other's dequant VALU. Accumulation order unchanged.
+  WO_STAG = 1 << 27
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -2069,27 +2073,34 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       for (int i = 0; i < FM; ++i) f.a[kc][i] = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
     }
   };
+  auto dq_half = [&](const Frag& f, int kc, v8h (&b)[FN]) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (BITS == 2) {
+        const uint32_t w = f.rb[j][0][0] >> (8 * kc);
+        b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j]);
+      } else if constexpr (BITS == 4) {
+        b[j] = wo_dequant<4>(&f.rb[j][0][kc], moff2, s2[j], z2[j]);
+      } else {
+        b[j] = wo_dequant<8>(f.rb[j][kc], moff2, s2[j], z2[j]);
+      }
+    }
+  };
+  auto mm_half = [&](const v8h (&a)[FM], const v8h (&b)[FN]) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[i][j], 0, 0, 0);
+  };
   auto mma_frag = [&](const Frag& f) {
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
       v8h b[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if constexpr (BITS == 2) {
-          const uint32_t w = f.rb[j][0][0] >> (8 * kc);
-          b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j]);
-        } else if constexpr (BITS == 4) {
-          b[j] = wo_dequant<4>(&f.rb[j][0][kc], moff2, s2[j], z2[j]);
-        } else {
-          b[j] = wo_dequant<8>(f.rb[j][kc], moff2, s2[j], z2[j]);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], f.a[kc][i], acc[i][j], 0, 0, 0);
+      dq_half(f, kc, b);
+      mm_half(f.a[kc], b);
     }
   };
+  constexpr bool STAG = PIPE && Cfg::BM == 64 && (WABL & WO_STAG) != 0;  // (128 rows: spills)
   if constexpr (PIPE) {
    if (nst > 0) {
     load_scales(ks0 / gstages, s2, z2);
@@ -2126,9 +2137,44 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
         }
       }
     };
-    for (int s = 0; s < nst; s += 2) {
-      step(s, fa, fb);
-      if (s + 1 < nst) step(s + 1, fb, fa);
+    if (!STAG || wave < 4) {
+      for (int s = 0; s < nst; s += 2) {
+        step(s, fa, fb);
+        if (s + 1 < nst) step(s + 1, fb, fa);
+      }
+    } else if constexpr (STAG) {
+      // late waves: stage s's second half (dequantised with stage s's scales before the barrier)
+      // runs after the barrier of iteration s+1, before stage s+2's reads reuse its register set
+      v8h bdef[FN];
+      auto step_late = [&](int s, Frag& cur, Frag& nxt) {
+        if (s + 1 < nst) {
+          if (s + DIST < nst) wait_vmcnt<(DIST - 2) * DPS>();
+          else wait_stage(nst - 2 - s);
+          lds_barrier();
+        }
+        if (s > 0) mm_half(nxt.a[1], bdef);  // stage s-1, second K half
+        const bool next_group = gpos == 0 && s + 1 < nst;
+        gpos = gpos + 1 == gstages ? 0 : gpos + 1;
+        if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);
+        if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
+        if (s + 1 < nst) read_frag((s + 1) % NBUF, nxt);
+        v8h b0[FN];
+        dq_half(cur, 0, b0);
+        mm_half(cur.a[0], b0);
+        dq_half(cur, 1, bdef);
+        if (next_group) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            s2[j] = s2n[j];
+            z2[j] = z2n[j];
+          }
+        }
+      };
+      for (int s = 0; s < nst; s += 2) {
+        step_late(s, fa, fb);
+        if (s + 1 < nst) step_late(s + 1, fb, fa);
+      }
+      mm_half(((nst - 1) & 1) ? fb.a[1] : fa.a[1], bdef);  // the last stage's second half
     }
     wait_vmcnt<0>();
     lds_barrier();  // ring -> epilogue staging
@@ -2218,17 +2264,17 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
     else if (cls == 1) gg_tile_v2<V2Cfg<128>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v2<V2Cfg<64>, QT_F16, ABL>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
-    constexpr int WABL = ABL & (kWoAblMask | WO_PIPE);
+    constexpr int WABL = ABL & (kWoAblMask | WO_PIPE | WO_STAG);
     if (cls == 0) gg_tile_wo<WoCfg<256>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_wo<WoCfg<64, 1>, 4, WABL>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
-    constexpr int WP = ABL & WO_PIPE;
+    constexpr int WP = ABL & (WO_PIPE | WO_STAG);
     if (cls == 0) gg_tile_wo<WoCfg<256>, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_wo<WoCfg<64, 1>, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) {
-    constexpr int WP = ABL & WO_PIPE;
+    constexpr int WP = ABL & (WO_PIPE | WO_STAG);
     if (cls == 0) gg_tile_wo<WoCfg<256>, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_wo<WoCfg<128, 1>, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_wo<WoCfg<64, 1>, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
