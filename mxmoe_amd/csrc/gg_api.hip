@@ -255,7 +255,10 @@ const std::vector<Variant>& variants() {
       // round 3 (AUTO default): v2s3's LDS image, buffer-form LDS-DMA spread over the first MFMA
       // group of each half stage, issued by waves 0-3 for their SIMD partners too (not on int4
       // tiles) — profiles/r03/lab/
-      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT)>("v2x_256x256_w8_b3_buf_spread_edma"),
+      // (+ the weight-only tiles' pipelined fragment reads and, at 64 rows, the late-wave deferral:
+      // +1-4 % on the small-batch w4a16 calls, profiles/r03/wo/)
+      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT) | WO_PIPE | WO_STAG>(
+          "v2x_256x256_w8_b3_buf_spread_edma"),
 #else
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
