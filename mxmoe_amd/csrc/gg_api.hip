@@ -872,6 +872,23 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   plan->tiles.resize(grid);
   plan->total_tiles = 0;
   for (const auto& q : queue) plan->total_tiles += (int)q.size();
+#ifdef MXMOE_LAB
+  // Low-fill LPT (lab opt-in, MXMOE_GG_LOWFILL_LPT=1): a call of at most 4 tiles per CU is laid out
+  // as one list in descending modelled tile time (stable: a tile's split-K slices and a band's
+  // m-tiles stay adjacent); block b then lands on XCD b % 8 and each XCD hands its sublist to its
+  // CUs in LPT order. At 2-3 tiles per CU the XCD chunks above concentrate the long tiles (the
+  // shared expert's split slices) on 2-3 XCDs, and the tile traces show 15-36 % ragged finish.
+  const char* lpt_env = planner_knob("MXMOE_GG_LOWFILL_LPT");
+  if (lpt_env && lpt_env[0] == '1' && v.kind == Kind::V2 && !v.persistent && plan->total_tiles <= 4 * 8 * chunk) {
+    std::vector<TileDesc> list;
+    for (const TileDesc& td : plan->tiles)
+      if (td.prob >= 0) list.push_back(td);
+    std::stable_sort(list.begin(), list.end(),
+                     [&](const TileDesc& a, const TileDesc& b) { return tile_time(a) > tile_time(b); });
+    plan->tiles = list;
+    grid = (int)list.size();
+  }
+#endif
   plan->launch_grid = grid;
   if (v.persistent) {
     // v2p: each XCD's queue handed out to its `chunk` workgroups in queue order, every tile to the
