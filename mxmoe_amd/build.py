@@ -30,13 +30,16 @@ def needs_build(lib: Path = LIB) -> bool:
     return any(p.stat().st_mtime > t for p in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None, lab: bool = False) -> Path:
+def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None, lab: bool = False,
+          lab_fast: bool = False) -> Path:
+    """lab_fast: the lab library with only the experiments under test (-DMXMOE_LAB_FAST; gg_api.hip)."""
+    lab = lab or lab_fast
     out = LAB_LIB if lab else LIB
     if not force and not needs_build(out):
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_suffix(".so.tmp")
-    defs = ["-DMXMOE_LAB"] if lab else []
+    defs = (["-DMXMOE_LAB"] if lab else []) + (["-DMXMOE_LAB_FAST"] if lab_fast else [])
     cmd = [HIPCC, *FLAGS, *defs, *(extra or []), "-o", str(tmp), *map(str, SOURCES)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -46,4 +49,4 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, lab="--lab" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose=True, lab="--lab" in sys.argv, lab_fast="--lab-fast" in sys.argv))

@@ -95,7 +95,16 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   } else if constexpr ((ABL & kWoAblMask) != 0) {
     launch_v2_q<ABL, 8>(a, grid, s);  // weight-only ablations: w4a16 tiles only
   } else {
-#ifdef MXMOE_LAB
+#if defined(MXMOE_LAB) && defined(MXMOE_LAB_FAST)
+    switch (qmask & 511) {
+      case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
+      case 2: launch_v2_q<ABL, 2>(a, grid, s); break;
+      case 8: launch_v2_q<ABL, 8>(a, grid, s); break;
+      default:
+        fprintf(stderr, "libmxmoe_gg_lab (fast): quant-type mix %#x not compiled\n", qmask);
+        abort();
+    }
+#elif defined(MXMOE_LAB)
     // lab build: fp16, w8a8, w4a4, w8a8 + w4a4 (LP-1 mixed), w4a16, bf16 only (fast builds)
     switch (qmask & 511) {
       case 1: launch_v2_q<ABL, 1>(a, grid, s); break;
@@ -167,6 +176,20 @@ void launch_v2p(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   }
 }
 
+template <int ABL, int QM, int NWG>
+void launch_wo2_q(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gg_wo2_kernel<ABL, QM, NWG>), dim3(grid), dim3(512), 0, s, a);
+}
+template <int ABL, int NWG>
+void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  switch (qmask & 511) {
+    case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;    // w4a16 only
+    case 16: launch_wo2_q<ABL, 16, NWG>(a, grid, s); break;  // w8a16 only
+    case 64: launch_wo2_q<ABL, 64, NWG>(a, grid, s); break;  // w2a16 only
+    default: launch_wo2_q<ABL, 88, NWG>(a, grid, s); break;  // any weight-only mix
+  }
+}
+
 template <class C16, class C8, class C4>
 Variant make_v0(const char* name) {
   Variant v;
@@ -223,6 +246,23 @@ Variant make_v2(const char* name) {
 }
 
 
+bool is_weightonly(int qt);
+
+// wo2: weight-only problems only, 64-row tiles, NWG workgroups per CU (gg_wo2_kernel)
+template <int ABL = 0, int NWG = 2>
+Variant make_wo2(const char* name) {
+  Variant v = make_v2<ABL>(name);
+  for (int q = 0; q < QT_COUNT; ++q)
+    if (!is_weightonly(q)) v.geom[q] = {0, 0, 0, 0};
+    else v.geom[q].bm = 64;
+  v.lds_bytes = wo2_lds_bytes<NWG>();
+  v.chunk = 32 * NWG;  // NWG workgroups per CU, 32 CUs per XCD
+  v.tail_bm = 0;
+  v.tail2_bm = 0;
+  v.launch = &launch_wo2<ABL, NWG>;
+  return v;
+}
+
 template <int TRACE = 0>
 Variant make_v2p(const char* name) {
   Variant v = make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT)>(name);
@@ -231,6 +271,10 @@ Variant make_v2p(const char* name) {
   v.launch = &launch_v2p<TRACE>;
   return v;
 }
+
+// the round-3 AUTO default's mainloop flags (variant v2x_256x256_w8_b3_buf_spread_edma, without the
+// weight-only options)
+constexpr int kV2x = V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT);
 
 typedef TileCfg<128, 128, 2, 2, 2> T128x128;
 typedef TileCfg<256, 128, 2, 2, 1> T256x128;
@@ -259,7 +303,19 @@ const std::vector<Variant>& variants() {
       // +1-4 % on the small-batch w4a16 calls, profiles/r03/wo/)
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT) | WO_PIPE | WO_STAG>(
           "v2x_256x256_w8_b3_buf_spread_edma"),
+#elif defined(MXMOE_LAB_FAST)
+      // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
+      // experiments under test only, fp16 / w8a8 bodies only
+      make_v2<kV2x>("x_v2x"),
+      make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
+      make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
+      make_v2<kV2x | V2_EPIPE | V2_LATEIL>("x_v2x_epipe_lateil"),
+      make_v2<kV2x | WO_PIPE | WO_STAG>("x_v2x_wo"),
+      make_wo2("x_wo2_64"),
+      make_wo2<0, 3>("x_wo3_64"),
 #else
+      make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
+      make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
       make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
       // mainloop experiments (correct results)

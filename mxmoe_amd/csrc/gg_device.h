@@ -597,7 +597,15 @@ enum : int {
   // with WO_PIPE: waves 4-7 defer each stage's second-K-half MFMAs (operands dequantised before
   // the barrier, held in registers) past the next barrier, so SIMD partners are half a stage
   // apart — one wave's MFMAs beside the other's dequant VALU. Accumulation order unchanged.
-  WO_STAG = 1 << 27
+  WO_STAG = 1 << 27,
+  // epilogue option: each wave writes fragment row i of its sub-tile into its LDS region, then
+  // reads back and stores fragment row i - 1 (16 rows), so the C stores start after one eighth of
+  // the scale / pack VALU instead of after all of it and drain under the rest
+  V2_EPIPE = 1 << 28,
+  // spread + EDMA option: the late waves interleave the A-fragment reads of the next K half into the
+  // current MFMA group (one read after the 4 MFMAs of each fragment row, which frees that row's
+  // registers), leaving only the B reads between the last MFMA and the barrier
+  V2_LATEIL = 1 << 29
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -1086,7 +1094,18 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           hread(fr, s, 0);
           hmma(fr);
           hread(fr, s, 1);
-          if constexpr (EDMA) {
+          if constexpr (EDMA && (ABL & V2_LATEIL) != 0 && Half::SUBH == 1) {
+            // {FN MFMAs of fragment row i, the next half's read of a[i]} x FM, then the FN B reads
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+#pragma unroll
+              for (int i = 0; i < FM; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              }
+              __builtin_amdgcn_sched_group_barrier(0x100, FN, 0);
+            }
+          } else if constexpr (EDMA) {
             __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
             __builtin_amdgcn_sched_group_barrier(0x008, NH, 0);
@@ -1322,8 +1341,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
     for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * e_g);
   }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
+  auto pack_row = [&](int i) {  // fragment row i (16 rows of the wave's sub-tile) -> LDS
     const int ml = i * 16 + e_r16;
     _Float16 sai = 0;
     if constexpr (qt_scaled(QT)) sai = sl[wm * Cfg::WTM + ml];
@@ -1336,12 +1354,11 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       const int q = 2 * j + (e_g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
     }
-  }
+  };
   _Float16* const cbase = C + (int64_t)mrow0 * mt.ldc + ncol0;  // wave-uniform
   const bool narrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;  // byte offsets < 2^30
   // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
-#pragma unroll 4
-  for (int it = 0; it < Cfg::WTM / 8; ++it) {
+  auto store_rows = [&](int it) {  // rows [8 it, 8 it + 8) of the wave's sub-tile, 16 B per lane
     const int row = it * 8 + (e_lane >> 3), q = e_lane & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 128 + ((q ^ (row & 7)) << 4));
     const int m = mrow0 + row, n = ncol0 + q * 8;
@@ -1350,6 +1367,25 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     } else {
       if (m < M && n < N) store_c16(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
     }
+  };
+  if constexpr ((ABL & V2_EPIPE) != 0) {
+    // stores of fragment row i - 1 issued behind the LDS writes of row i: the first 2 KiB of the
+    // wave's 16 KiB leave after one eighth of the pack VALU, the rest drain under the remaining rows
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      pack_row(i);
+      if (i > 0) {
+        store_rows(2 * i - 2);
+        store_rows(2 * i - 1);
+      }
+    }
+    store_rows(2 * FM - 2);
+    store_rows(2 * FM - 1);
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) pack_row(i);
+#pragma unroll 4
+    for (int it = 0; it < Cfg::WTM / 8; ++it) store_rows(it);
   }
 }
 
@@ -1832,7 +1868,7 @@ __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2
 // WM_ = waves along M: 2 for 256-row tiles; 1 for the 128 / 64-row classes, so that each B
 // fragment is dequantised by exactly one wave and reused over all its 4-8 A fragments (with 2 x 4
 // waves and 32-row wave tiles the dequant VALU outweighed the MFMAs 11:1 at small batch)
-template <int BM_, int WM_ = 2>
+template <int BM_, int WM_ = 2, int LDSB_ = V2Cfg<256>::LDS_BYTES>
 struct WoCfg {
   static constexpr int BM = BM_, BN = 256, NT = 512, KS = 64;  // KS: K elements per stage
   static constexpr int WM = WM_, WN = 8 / WM_;
@@ -1848,9 +1884,10 @@ struct WoCfg {
   static constexpr int stage_bytes() { return A_BYTES + BN * KS * BITS / 8; }
   template <int BITS>
   static constexpr int nbuf() {
-    return V2Cfg<256>::LDS_BYTES / stage_bytes<BITS>() > 8 ? 8 : V2Cfg<256>::LDS_BYTES / stage_bytes<BITS>();
+    return LDSB_ / stage_bytes<BITS>() > 8 ? 8 : LDSB_ / stage_bytes<BITS>();
   }
-  static_assert(2 * STAGE_BYTES <= V2Cfg<256>::LDS_BYTES, "two stages must fit the v2 LDS image");
+  static_assert(2 * STAGE_BYTES <= LDSB_, "two stages must fit the LDS image");
+  static_assert(WM * WN * WTM * WTN * 2 <= LDSB_, "the epilogue's staged tile must fit the LDS image");
 };
 
 __device__ __forceinline__ uint32_t wo_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
@@ -2291,6 +2328,44 @@ __global__ __launch_bounds__(512, 2) void gg_v2_kernel(GGArgs args) {
   }
 }
 
+
+// ============================================================================================
+// wo2: the 64-row weight-only tile (gg_tile_wo, 1 x 8 waves, 64 x 32 wave tiles) in a kernel small
+// enough for TWO workgroups per CU: <= 128 VGPRs (4 waves per SIMD) and a 78-KiB LDS image (ring
+// of 4 stages for 4-bit codes, 3 for 8-bit, 6 for 2-bit; the 32-KiB epilogue staging). For small
+// batches (routed experts of ~35 rows) the 64-row tile is bound by its per-stage instruction
+// stream and barrier latency, not by the weight stream: a second resident workgroup fills the
+// other one's waits. Planned with 64-row tiles only (variant geometry bm = 64, no tail classes).
+// ============================================================================================
+// NWG = 3: three workgroups per CU (<= 80 VGPRs, 52-KiB image: 3 / 2 / 4 stages)
+template <int NWG>
+constexpr int wo2_lds_bytes() { return NWG == 3 ? 52 * 1024 : 78 * 1024; }
+template <int ABL, int QM, int NWG = 2>
+__global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
+  constexpr int WO2_LDS_BYTES = wo2_lds_bytes<NWG>();
+  __shared__ __attribute__((aligned(16))) uint8_t lds[WO2_LDS_BYTES];
+  const TileDesc td = args.tiles[blockIdx.x];
+  if (td.prob < 0) return;
+  const GGMeta mt = args.meta[td.prob];
+  const uint8_t* A = static_cast<const uint8_t*>(args.ptr_A[td.prob]);
+  const uint8_t* B = static_cast<const uint8_t*>(args.ptr_B[td.prob]);
+  const _Float16* SB = static_cast<const _Float16*>(args.ptr_SB[td.prob]);
+  _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
+  SplitK sk;
+  sk.ks0 = td.ks0;
+  sk.nst = td.ks1 - td.ks0;
+  sk.idx = (td.cls >> 8) & 0xFF;
+  sk.nsplit = (td.cls >> 16) & 0xFF;
+  sk.slab = td.slab;
+  sk.grp = td.grp;
+  sk.slabs = args.slabs;
+  sk.counters = args.counters;
+  typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG);
+  if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+}
 
 // ============================================================================================
 // v2p: the persistent v2x. One 512-thread workgroup per CU walks a planned list of tiles

@@ -114,7 +114,7 @@ def main():
             samples[k].append(t["median_ms"])
     for gg, ts, lab in zip(ggs, samples, labels):
         med = statistics.median(ts)
-        print(json.dumps({"variant": gg.variant, "spec": lab, "cfg": args.cfg, "gg": args.gg, "only": args.only,
+        print(json.dumps({"variant": gg.variant, "spec": lab, "cfg": args.cfg, "gg": args.gg, "bs": args.bs, "only": args.only,
                           "median_ms": round(med, 4), "spread_ms": round(max(ts) - min(ts), 4),
                           "tiles": gg.total_tiles, "grid": gg.info.grid,
                           "tflops": round(inp.flops / (med * 1e-3) / 1e12, 1),

@@ -49,13 +49,17 @@ def cases():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="")
+    ap.add_argument("--cases", default="", help="comma list of case-name prefixes (fast lab: fp16,w8a8)")
     args = ap.parse_args()
+    prefixes = tuple(c for c in args.cases.split(",") if c)
     names = {int(ln.split()[0]): ln.split()[1] for ln in nat.list_variants()}
     vs = [int(v) for v in args.variants.split(",")] if args.variants else \
         [i for i, n in names.items() if not n.startswith("abl_")]
     bad = 0
     for v in vs:
         for case, specs in cases():
+            if prefixes and not case.startswith(prefixes):
+                continue
             hps = [HostProblem(M, N, K, q, seed=31 + i, device="cuda") for i, (M, N, K, q) in enumerate(specs)]
             group_gemm([h.problem for h in hps], variant=v)
             torch.cuda.synchronize()
