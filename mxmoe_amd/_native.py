@@ -187,9 +187,12 @@ def variant_count() -> int:
     return lib().mxmoe_gg_variant_count()
 
 
-def production_variants() -> list[int]:
-    """Compiled variants that compute correct results (``abl_*`` are timing ablations)."""
-    return [int(ln.split()[0]) for ln in list_variants() if not ln.split()[1].startswith("abl_")]
+def production_variants(qcfg: str | None = "fp16") -> list[int]:
+    """Compiled variants that compute correct results (``abl_*`` are timing ablations) and have a tile
+    body for ``qcfg`` (default fp16: the general-purpose kernels; ``None``: every one, including the
+    weight-only-only ``wo3_*``)."""
+    vs = [int(ln.split()[0]) for ln in list_variants() if not ln.split()[1].startswith("abl_")]
+    return vs if qcfg is None else [v for v in vs if variant_supports(v, qcfg)]
 
 
 def plan_tiles(problems, variant: int):

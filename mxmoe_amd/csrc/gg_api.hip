@@ -184,9 +184,11 @@ template <int ABL, int NWG>
 void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {
     case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;    // w4a16 only
-    case 16: launch_wo2_q<ABL, 16, NWG>(a, grid, s); break;  // w8a16 only
     case 64: launch_wo2_q<ABL, 64, NWG>(a, grid, s); break;  // w2a16 only
-    default: launch_wo2_q<ABL, 88, NWG>(a, grid, s); break;  // any weight-only mix
+    // the 8-bit body does not fit 80 VGPRs (3 workgroups per CU) without spilling: calls with w8a16
+    // problems run the 2-WG/CU build of the same tiles (same plan: placement only assumes more slots)
+    case 16: launch_wo2_q<ABL, 16, 2>(a, grid, s); break;  // w8a16 only
+    default: launch_wo2_q<ABL, 88, 2>(a, grid, s); break;  // any weight-only mix
   }
 }
 
@@ -301,8 +303,10 @@ const std::vector<Variant>& variants() {
       // tiles) — profiles/r03/lab/
       // (+ the weight-only tiles' pipelined fragment reads and, at 64 rows, the late-wave deferral:
       // +1-4 % on the small-batch w4a16 calls, profiles/r03/wo/)
-      make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT) | WO_PIPE | WO_STAG>(
-          "v2x_256x256_w8_b3_buf_spread_edma"),
+      make_v2<kV2x | WO_PIPE | WO_STAG>("v2x_256x256_w8_b3_buf_spread_edma"),
+      // round 3 (AUTO for small-batch weight-only calls): the 64-row weight-only tile at three
+      // workgroups per CU (gg_wo2_kernel<.., 3>; weight-only problems only) — profiles/r03/wo2/
+      make_wo2<0, 3>("wo3_64x256_w8_3wg"),
 #elif defined(MXMOE_LAB_FAST)
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
       // experiments under test only, fp16 / w8a8 bodies only
@@ -361,6 +365,11 @@ const std::vector<Variant>& variants() {
 // (v3), unless they are low-fill enough to need split-K (v2 kernels only).
 constexpr const char* kDefaultVariantName = "v2x_256x256_w8_b3_buf_spread_edma";
 constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
+constexpr const char* kWoSmallVariant = "wo3_64x256_w8_3wg";
+// weight-only calls whose rows per weight byte are this small or smaller run kWoSmallVariant:
+// the weight-bytes-weighted mean M over the call's problems (qwen2_moe layer 11: ~60 at bs = 128,
+// ~250 at bs = 2048, ~1030 at bs = 8192, where v2x's 256-row tiles are as fast or faster)
+constexpr double kWoSmallMeanRows = 512.0;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
@@ -615,7 +624,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
         biggest[i] = std::max(biggest[i], c);
       }
     }
-    const double share = total / kSplitCUs;
+    const double share = total / (kSplitCUs * v.chunk / 32);  // workgroup slots: CUs x workgroups per CU
     for (int i : order) {
       const double ratio = biggest[i] / std::max(share, 1.0);
       // (w4a4 g128 never splits: summing f32 partial folds would change the rounding)
@@ -993,6 +1002,25 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     if (p.M > 0 && qtype_of(p.a_bits, p.w_bits, p.gsize, p.sym, p.fmt, &qt) == MXMOE_GG_OK) mask |= 1 << qt;
   }
   *out = variant_index(kDefaultVariantName);
+  const int wo_mask = (1 << QT_W4A16) | (1 << QT_W8A16) | (1 << QT_W2A16);
+  if (mask != 0 && (mask & ~wo_mask) == 0) {
+    // weight-only: the 3-WG/CU 64-row kernel while the rows per weight byte are few (small batches:
+    // the 64-row tile is bound by its instruction stream and barriers, a second and third resident
+    // workgroup fill each other's waits — +15-70 % on the qwen2_moe calls at bs 128-2048,
+    // profiles/r03/wo2/); v2x's 256-row tiles at large batch
+    double wsum = 0, msum = 0;
+    for (const HostProblem& p : hp) {
+      if (p.M <= 0 || p.N <= 0) continue;
+      const double w = (double)p.N * p.K;
+      wsum += w;
+      msum += w * p.M;
+    }
+    if (wsum > 0 && msum / wsum <= kWoSmallMeanRows) {
+      const int wi = variant_index(kWoSmallVariant);
+      if (!strcmp(variants()[wi].name, kWoSmallVariant)) *out = wi;
+    }
+    return MXMOE_GG_OK;
+  }
   if (mask == (1 << QT_I4)) {
     // int4-only: the 256x128 2-WG/CU kernel, unless the call is low-fill enough for the v2s plan
     // to split K (that kernel cannot)

@@ -120,7 +120,7 @@ def main(argv=None):
             tiles = parse_tile_config_json(args.tile_config, qcfg_list, layer)
             variants = [select_variant(tiles, nat.default_variant())]
         else:  # every compiled variant that has a tile body for each qcfg of the layer
-            variants = [v for v in nat.production_variants() if all(nat.variant_supports(v, q) for q in qcfg_list)]
+            variants = [v for v in nat.production_variants(None) if all(nat.variant_supports(v, q) for q in qcfg_list)]
         names = nat.list_variants()
         result["variants"][layer] = variants
         parsed = load_workload(wl)[f"layer-{layer}"]

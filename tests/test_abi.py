@@ -105,6 +105,33 @@ def test_auto_variant_is_v2x_at_every_k():
             assert auto(probs) == nat.default_variant(), (bs, gg)
 
 
+def test_auto_variant_weightonly_small_batch_runs_wo3():
+    """AUTO (round 3): a call of weight-only problems only runs wo3 (64-row tiles, 3 workgroups per
+    CU) while the weight-bytes-weighted mean M is <= 512 rows, v2x above; any other quant type in the
+    call keeps v2x (wo3 has no fp16 / int tile body)."""
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    wo3 = names.index("wo3_64x256_w8_3wg")
+
+    def auto(ps):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.resolve_variant(arr, len(ps))
+
+    from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
+
+    for qstr in ("w4a16_g128_asym", "w4a16_g-1_sym", "w8a16_g-1_asym", "w2a16_g128_asym"):
+        bits, g, sym = int(qstr[1]), int(qstr.split("_g")[1].split("_")[0]), qstr.endswith("_sym")
+        wo = dict(a_bits=16, w_bits=bits, gsize=g, sym=int(sym), scale_a=0)
+        for bs, want in ((128, wo3), (512, wo3), (2048, wo3), (8192, nat.default_variant())):
+            layer = load_workload(qwen2_layer11_workload(bs, qstr=qstr))["layer-11"]
+            for gg in ("gate_up", "down"):
+                probs = [_prob(M=s.M, N=s.N, K=s.K, **wo) for s in layer[gg]]
+                assert auto(probs) == want, (qstr, bs, gg)
+                mixed = probs + [_prob(M=64, N=256, K=layer[gg][0].K)]  # + one w8a8 problem
+                assert auto(mixed) == nat.default_variant(), (qstr, bs, gg)
+    assert not nat.variant_supports(wo3, "fp16") and not nat.variant_supports(wo3, "w8a8_g-1_sym")
+    assert wo3 not in nat.production_variants() and wo3 in nat.production_variants("w4a16_g128_asym")
+
+
 def _plan(problems, ws_bytes=1 << 20):
     arr = (nat.GGProblemC * len(problems))(*problems)
     info = nat.GGPlanInfo()

@@ -40,8 +40,9 @@ def test_hip_matches_reference_fake_quant(kind, variant):
         assert_fakequant_close(p.C[: p.M, : p.N].cpu().numpy(), r, f"{kind} M={p.M} N={p.N} K={p.K}")
 
 
+@pytest.mark.parametrize("variant", [None] + nat.production_variants("w4a16_g-1_asym"))  # None: AUTO
 @pytest.mark.parametrize("ref_format", [False, True], ids=["mi355x_layout", "reference_packed_repack"])
-def test_weightonly_hip_matches_reference_fake_quant(ref_format):
+def test_weightonly_hip_matches_reference_fake_quant(ref_format, variant):
     probs, refs = [], []
     for i, M, N, K, bits, gsize, sym, fq in wo_problems():
         q, sz = weightonly.quant_wo(fq[f"wo{i}_B"], bits, gsize, sym)  # == the reference's quant_minmax
@@ -54,7 +55,7 @@ def test_weightonly_hip_matches_reference_fake_quant(ref_format):
                              M=M, N=N, K=K, q=QParams(16, bits, gsize, sym),
                              scale_b=torch.from_numpy(weightonly.permute_scale(sz, N, K, gsize, sym)).to(DEV)))
         refs.append(fq[f"wo{i}_Cfq"])
-    group_gemm(probs)
+    group_gemm(probs, variant=variant)
     torch.cuda.synchronize()
     for p, r in zip(probs, refs):
         assert_fakequant_close(p.C[: p.M, : p.N].cpu().numpy(), r, f"{p.q.qcfg} M={p.M} N={p.N} K={p.K}")
@@ -89,7 +90,8 @@ def _w4a16_w8a8_problems():
     return probs, refs, exact
 
 
-@pytest.mark.parametrize("variant", [v for v in nat.production_variants() if nat.variant_supports(v, "w4a16_g-1_asym")])
+@pytest.mark.parametrize("variant", [v for v in nat.production_variants("w4a16_g-1_asym")
+                                     if nat.variant_supports(v, "w8a8_g-1_sym")])
 def test_w4a16_w8a8_fused_launch_matches_reference_fake_quant(variant):
     probs, refs, exact = _w4a16_w8a8_problems()
     group_gemm(probs, variant=variant)

@@ -30,7 +30,7 @@ def _gpu():
 
 
 def _variants(qcfg):
-    return [v for v in nat.production_variants() if nat.variant_supports(v, qcfg)]
+    return nat.production_variants(qcfg)
 
 
 def _check(hps):

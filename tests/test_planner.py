@@ -144,7 +144,7 @@ def test_product_plan_ignores_planner_ab_switches(monkeypatch, cfg):
 def test_product_library_lists_only_correct_variants():
     names = [ln.split()[1] for ln in nat.list_variants()]
     assert names and not any(n.startswith(("abl_", "x_")) for n in names)
-    assert nat.production_variants() == list(range(len(names)))
+    assert nat.production_variants(None) == list(range(len(names)))
 
 
 def test_routed_experts_stay_on_one_xcd():

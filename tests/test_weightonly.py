@@ -101,6 +101,9 @@ def test_weightonly_only_on_v2_variants():
         if name.startswith(("v2", "abl_v2")):
             assert st == nat.MXMOE_GG_ERR_WORKSPACE, (name, err)  # validation passed, no workspace given
             assert "w4a16=TileConfig(BM=256, BN=256, BK=64" in ln and "w8a16=TileConfig(" in ln
+        elif name.startswith("wo3"):  # weight-only-only kernel: 64-row tiles, no fp16 / int bodies
+            assert st == nat.MXMOE_GG_ERR_WORKSPACE, (name, err)
+            assert "w4a16=TileConfig(BM=64, BN=256, BK=64" in ln and "fp16=" not in ln
         else:
             assert st == nat.MXMOE_GG_ERR_UNSUPPORTED and "does not implement" in err, name
             assert "w4a16" not in ln

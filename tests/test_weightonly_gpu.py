@@ -12,6 +12,8 @@ from tests._util import HostProblem, assert_f16_close
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 V2 = [int(ln.split()[0]) for ln in nat.list_variants() if ln.split()[1].startswith("v2")]
+# weight-only-only kernels (wo3: 64-row tiles, 3 workgroups per CU)
+WO = [v for v in nat.production_variants("w4a16_g-1_asym") if not nat.variant_supports(v, "fp16")]
 QS = [QParams(16, b, g, s) for b in (2, 4, 8) for g in (-1, 128) for s in (True, False)]
 
 
@@ -21,7 +23,7 @@ def _check(hps):
             assert_f16_close(hp.result(), hp.expected(), hp.K)
 
 
-@pytest.mark.parametrize("variant", V2)
+@pytest.mark.parametrize("variant", V2 + WO)
 @pytest.mark.parametrize("q", QS, ids=[q.qcfg for q in QS])
 def test_weightonly_edge_shapes(q, variant):
     shapes = [(1, 128, 256), (17, 256, 128 if q.gsize == -1 else 256), (130, 136, 384), (257, 264, 512),
@@ -54,6 +56,30 @@ def test_all_quant_types_in_one_launch(variant):
     gg.launch()
     torch.cuda.synchronize()
     _check(hps)
+
+
+@pytest.mark.parametrize("variant", WO)
+def test_wo3_weightonly_mix_and_split_k(variant):
+    """Every weight-only width in one wo3 launch (the QM = 88 specialisation), plus a low-fill call
+    whose long-K problem the planner splits along K (slab reduce in the 3-WG/CU kernel)."""
+    assert WO, "no weight-only-only variant compiled"
+    specs = [(260, 256, 1408, QParams(16, 4, 128, False)), (33, 512, 2048, QParams(16, 8, -1, True)),
+             (0, 256, 256, QParams(16, 4, -1, True)), (513, 264, 640, QParams(16, 4, 64, True)),
+             (96, 256, 512, QParams(16, 2, 128, False)), (7, 136, 1024, QParams(16, 8, 128, False))]
+    hps = [HostProblem(M, N, K, q, seed=90 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
+    gg = GroupGemm([h.problem for h in hps], variant=variant)
+    gg.launch()
+    torch.cuda.synchronize()
+    _check(hps)
+    # low fill: one 128 x 2048 x 5632 problem (the bs=128 shared-expert down shape) + 4 small ones
+    hps = [HostProblem(128, 2048, 5632, QParams(16, 4, 128, False), seed=95, device=DEV)] + \
+          [HostProblem(9, 2048, 1408, QParams(16, 4, 128, False), seed=96 + i, device=DEV) for i in range(4)]
+    gg = GroupGemm([h.problem for h in hps], variant=variant)
+    assert gg.info.splitk_slabs > 0, "expected a split-K plan"
+    for _ in range(2):  # counters re-armed between launches
+        gg.launch()
+        torch.cuda.synchronize()
+        _check(hps)
 
 
 @pytest.mark.parametrize("bs", [512, 128])

@@ -25,7 +25,8 @@ from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_w
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfg", default="mixed", choices=["mixed", "ds2_mixed"])
+    ap.add_argument("--cfg", default="mixed", choices=["mixed", "ds2_mixed", "w4a16_w8a8"])
+    ap.add_argument("--bs", type=int, default=8192)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
@@ -33,13 +34,17 @@ def main():
         if args.cfg == "ds2_mixed":
             from mxmoe_amd.workload import ds2_mixed_qconfig, ds2_workload
 
-            shapes = load_workload(ds2_workload(8192, qconfig=ds2_mixed_qconfig()))["layer-1"][gg_name]
+            shapes = load_workload(ds2_workload(args.bs, qconfig=ds2_mixed_qconfig()))["layer-1"][gg_name]
+        elif args.cfg == "w4a16_w8a8":  # split: weight-only problems (-> wo3 at small batch) vs w8a8
+            from mxmoe_amd.workload import w4a16_w8a8_qconfig
+
+            shapes = load_workload(qwen2_layer11_workload(args.bs, qconfig=w4a16_w8a8_qconfig()))["layer-11"][gg_name]
         else:
-            shapes = load_workload(qwen2_layer11_workload(8192, qconfig=mixed_qconfig_lp1()))["layer-11"][gg_name]
+            shapes = load_workload(qwen2_layer11_workload(args.bs, qconfig=mixed_qconfig_lp1()))["layer-11"][gg_name]
         inp = build_layer_inputs(shapes)
         probs = inp.problems
         p8 = [p for p, s in zip(probs, shapes) if s.a_bits == 8]
-        p4 = [p for p, s in zip(probs, shapes) if s.a_bits == 4]
+        p4 = [p for p, s in zip(probs, shapes) if s.a_bits == (16 if args.cfg == "w4a16_w8a8" else 4)]
         fused = GroupGemm(probs)
         g8, g4 = GroupGemm(p8), GroupGemm(p4)
         main_s = torch.cuda.current_stream()
