@@ -370,7 +370,7 @@ def main():
     ap.add_argument("--dist-extras-all", action="store_true",
                     help="N > 1: also run the N-slice strong-scaling and EP weak-scaling extras (off by default: "
                          "the default N > 1 run exercises one RCCL path, the expert split)")
-    ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed,w4a16_w8a8_bs512", help="other configs measured as extra fields (N=1)")
+    ap.add_argument("--extras", default="w8a8,w4a4,mixed,ds2_mixed,w4a16_w8a8_bs512,w4a16_bs512", help="other configs measured as extra fields (N=1)")
     ap.add_argument("--median-iters", type=int, default=50)
     ap.add_argument("--dist-extras", default="ds2_mixed", help="other configs run through the expert split at N > 1")
     ap.add_argument("--extras-warmup", type=int, default=200, help="untimed steps before an extra config's launch timing")
