@@ -185,10 +185,11 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {
     case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;    // w4a16 only
     case 64: launch_wo2_q<ABL, 64, NWG>(a, grid, s); break;  // w2a16 only
+    case 10: launch_wo2_q<ABL, 10, NWG>(a, grid, s); break;  // w4a16 + w8a8 (hz_fused pairing)
     // the 8-bit body does not fit 80 VGPRs (3 workgroups per CU) without spilling: calls with w8a16
     // problems run the 2-WG/CU build of the same tiles (same plan: placement only assumes more slots)
     case 16: launch_wo2_q<ABL, 16, 2>(a, grid, s); break;  // w8a16 only
-    default: launch_wo2_q<ABL, 88, 2>(a, grid, s); break;  // any weight-only mix
+    default: launch_wo2_q<ABL, 90, 2>(a, grid, s); break;  // any mix of weight-only and w8a8
   }
 }
 
@@ -257,6 +258,7 @@ Variant make_wo2(const char* name) {
   for (int q = 0; q < QT_COUNT; ++q)
     if (!is_weightonly(q)) v.geom[q] = {0, 0, 0, 0};
     else v.geom[q].bm = 64;
+  v.geom[QT_I8] = {64, 128, 128, 512};  // w8a8 beside weight-only problems: 64 x 128 int8 tiles
   v.lds_bytes = wo2_lds_bytes<NWG>();
   v.chunk = 32 * NWG;  // NWG workgroups per CU, 32 CUs per XCD
   v.tail_bm = 0;
@@ -1003,7 +1005,8 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   }
   *out = variant_index(kDefaultVariantName);
   const int wo_mask = (1 << QT_W4A16) | (1 << QT_W8A16) | (1 << QT_W2A16);
-  if (mask != 0 && (mask & ~wo_mask) == 0) {
+  if ((mask & wo_mask) != 0 && (mask & ~(wo_mask | (1 << QT_I8))) == 0) {
+    // (w8a8 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
     // weight-only: the 3-WG/CU 64-row kernel while the rows per weight byte are few (small batches:
     // the 64-row tile is bound by its instruction stream and barriers, a second and third resident
     // workgroup fill each other's waits — +15-70 % on the qwen2_moe calls at bs 128-2048,

@@ -399,10 +399,10 @@ __global__ __launch_bounds__(C16::kThreads, C16::kMinWavesPerEU) void gg_fused_k
 //   * epilogue: each wave stages its own fp16 sub-tile in LDS (XOR-swizzled 16-B chunks) and
 //     stores full 128-B row segments with 16-B stores.
 // ============================================================================================
-template <int BM_>
+template <int BM_, int BN_ = 256, int WM_ = 2, int WN_ = 4>
 struct V2Cfg {
-  static constexpr int BM = BM_, BN = 256, NT = 512, BKB = 128;
-  static constexpr int WM = 2, WN = 4;
+  static constexpr int BM = BM_, BN = BN_, NT = 512, BKB = 128;
+  static constexpr int WM = WM_, WN = WN_;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
   static constexpr int A_BYTES = BM * BKB, B_BYTES = BN * BKB, STAGE_BYTES = A_BYTES + B_BYTES;
@@ -2362,7 +2362,13 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
   constexpr int WP = ABL & (WO_PIPE | WO_STAG);
-  if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
+    // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
+    // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
+    // (two 24-KiB stages + the scale stash: 49 KiB)
+    const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
+    gg_tile_v2<V2Cfg<64, 128, 4, 2>, QT_I8, 0>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+  } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
 }

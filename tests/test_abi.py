@@ -106,9 +106,10 @@ def test_auto_variant_is_v2x_at_every_k():
 
 
 def test_auto_variant_weightonly_small_batch_runs_wo3():
-    """AUTO (round 3): a call of weight-only problems only runs wo3 (64-row tiles, 3 workgroups per
-    CU) while the weight-bytes-weighted mean M is <= 512 rows, v2x above; any other quant type in the
-    call keeps v2x (wo3 has no fp16 / int tile body)."""
+    """AUTO (round 3): a call of weight-only problems (w8a8 problems may ride along: the reference's
+    small-batch w4a16 + w8a8 pairing) runs wo3 (64-row tiles, 3 workgroups per CU) while the
+    weight-bytes-weighted mean M is <= 512 rows, v2x above; fp16 / w4a4 problems in the call, or no
+    weight-only problem at all, keep v2x (wo3 has no fp16 / int4 tile body)."""
     names = [ln.split()[1] for ln in nat.list_variants()]
     wo3 = names.index("wo3_64x256_w8_3wg")
 
@@ -126,9 +127,14 @@ def test_auto_variant_weightonly_small_batch_runs_wo3():
             for gg in ("gate_up", "down"):
                 probs = [_prob(M=s.M, N=s.N, K=s.K, **wo) for s in layer[gg]]
                 assert auto(probs) == want, (qstr, bs, gg)
-                mixed = probs + [_prob(M=64, N=256, K=layer[gg][0].K)]  # + one w8a8 problem
-                assert auto(mixed) == nat.default_variant(), (qstr, bs, gg)
-    assert not nat.variant_supports(wo3, "fp16") and not nat.variant_supports(wo3, "w8a8_g-1_sym")
+                K = layer[gg][0].K
+                assert auto(probs + [_prob(M=64, N=256, K=K)]) == want, (qstr, bs, gg)  # + a w8a8 problem
+                f16 = _prob(M=64, N=256, K=K, a_bits=16, w_bits=16, scale_a=0, scale_b=0)
+                assert auto(probs + [f16]) == nat.default_variant(), (qstr, bs, gg)
+                assert auto(probs + [_prob(M=64, N=256, K=K, a_bits=4, w_bits=4)]) == nat.default_variant()
+    assert auto([_prob(M=64, N=256, K=1024)]) == nat.default_variant()  # w8a8 alone: v2x
+    assert not nat.variant_supports(wo3, "fp16") and not nat.variant_supports(wo3, "w4a4_g-1_sym")
+    assert nat.variant_supports(wo3, "w8a8_g-1_sym")
     assert wo3 not in nat.production_variants() and wo3 in nat.production_variants("w4a16_g128_asym")
 
 

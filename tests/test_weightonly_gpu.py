@@ -82,8 +82,29 @@ def test_wo3_weightonly_mix_and_split_k(variant):
         _check(hps)
 
 
+@pytest.mark.parametrize("variant", WO)
+def test_wo3_w8a8_beside_weightonly_bit_exact(variant):
+    """wo3's int8 body (64 x 128 tiles, plain v2 mainloop) beside weight-only problems: w8a8 edge
+    shapes (M 1 / 17 / 130, N tails, K tails inside a 128-B stage, long K) bit-exact against the
+    oracle in one launch with w4a16 problems; then the same with split-K (low fill, long K)."""
+    specs = [(1, 128, 256, W8A8), (17, 136, 128, W8A8), (130, 264, 384 + 48, W8A8), (300, 520, 512, W8A8),
+             (64, 8, 1024 + 16, W8A8), (77, 256, 1408, QParams(16, 4, -1, False)), (34, 2816, 2048, W8A8)]
+    hps = [HostProblem(M, N, K, q, seed=110 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
+    for _ in range(2):
+        GroupGemm([h.problem for h in hps], variant=variant).launch()
+        torch.cuda.synchronize()
+        for h in hps:
+            if h.q.is_weight_only:
+                assert_f16_close(h.result(), h.expected(), h.K)
+            else:
+                assert (h.result().view(np.uint16) == h.expected().view(np.uint16)).all(), (h.M, h.N, h.K)
+        hps = [HostProblem(40, 1024, 8192, W8A8, seed=120, device=DEV),
+               HostProblem(20, 512, 1024, QParams(16, 4, 128, False), seed=121, device=DEV)]
+
+
+@pytest.mark.parametrize("variant", [None] + WO)  # None: AUTO (wo3 at these batches)
 @pytest.mark.parametrize("bs", [512, 128])
-def test_w4a16_w8a8_layer_bs512_matches_oracle(bs):
+def test_w4a16_w8a8_layer_bs512_matches_oracle(bs, variant):
     """BASELINE's small-batch mixed scheme (bench config w4a16_w8a8_bs512): the qwen2_moe layer-11
     gate_up and down calls at bs = 512 with 1/16 of the blocks w8a8 and the rest w4a16_g-1_asym, ONE
     fused AUTO launch each; every problem against the oracle on a row / column sample (w8a8 bit-exact,
@@ -97,7 +118,7 @@ def test_w4a16_w8a8_layer_bs512_matches_oracle(bs):
         assert {s.qcfg for s in shapes} == {"w4a16_g-1_asym", "w8a8_g-1_sym"}
         hps = [HostProblem(s.M, s.N, s.K, QParams(s.a_bits, s.w_bits, s.gsize, s.sym), seed=500 + i, device=DEV)
                for i, s in enumerate(shapes)]
-        GroupGemm([h.problem for h in hps]).launch()
+        GroupGemm([h.problem for h in hps], variant=variant).launch()
         torch.cuda.synchronize()
         for h in hps:
             if h.M == 0:
