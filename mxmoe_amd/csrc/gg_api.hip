@@ -632,6 +632,12 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       // (w4a4 g128 never splits: summing f32 partial folds would change the rounding)
       if (ratio > 2.0 && all[i].qtype != QT_I4G) split[i] = std::max(1, std::min({8, (int)ratio, stages_of(all[i]) / 4}));
     }
+    // lab A/B switch: every problem split into at least S K slices (where it has >= 4 S stages)
+    const char* sall = planner_knob("MXMOE_GG_SPLITK_ALL");
+    if (sall && atoi(sall) > 1)
+      for (int i : order)
+        if (all[i].qtype != QT_I4G)
+          split[i] = std::max(split[i], std::max(1, std::min({8, atoi(sall), stages_of(all[i]) / 4})));
   }
   // Tile time model (per K stage, in "bytes": one stage's LDS-DMA bytes or its MFMA work at the
   // fp16 rate of 128 flop/B, whichever is larger, plus a fixed 24 KiB-equivalent per stage).
