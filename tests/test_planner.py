@@ -72,15 +72,21 @@ def check_coverage(shapes, variant=nat.VARIANT_AUTO):
     return tiles, rows, v
 
 
-@pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed", "e4m3", "w4a16"])
-@pytest.mark.parametrize("bs", [8192, 512])
+@pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed", "e4m3", "w4a16", "w4a16_w8a8", "w2a16", "w8a16"])
+@pytest.mark.parametrize("bs", [8192, 512, 128])
 def test_every_tile_planned_once(cfg, bs):
+    from mxmoe_amd.workload import w4a16_w8a8_qconfig
+
     kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
           "mixed": dict(qconfig=mixed_qconfig_lp1()), "e4m3": dict(qstr="w8a8_g-1_sym_E4M3"),
-          "w4a16": dict(qstr="w4a16_g128_asym")}[cfg]
+          "w4a16": dict(qstr="w4a16_g128_asym"), "w4a16_w8a8": dict(qconfig=w4a16_w8a8_qconfig()),
+          "w2a16": dict(qstr="w2a16_g128_asym"), "w8a16": dict(qstr="w8a16_g-1_asym")}[cfg]
     layer = _layer(bs, **kw)
+    names = [ln.split()[1] for ln in nat.list_variants()]
     for gg in ("gate_up", "down"):
-        check_coverage(layer[gg])
+        _, _, v = check_coverage(layer[gg])
+        # (small-batch weight-only calls, w8a8 riding along, plan for the 3-WG/CU kernel)
+        assert (names[v] == "wo3_64x256_w8_3wg") == (cfg in ("w4a16", "w4a16_w8a8", "w2a16", "w8a16") and bs < 8192)
 
 
 def test_other_models_and_every_v2_variant():
