@@ -147,18 +147,18 @@ void launch_v2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
 }
 
 // v3 is specialised on the set of quant types the plan contains (mask 1 << QType)
-template <int BN, int WN, int NBUF, int DIST, int QM>
+template <int BN, int WN, int NBUF, int DIST, int QM, int OPT>
 void launch_v3_q(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gg_v3_kernel<BN, WN, NBUF, DIST, QM>), dim3(grid), dim3(V3Cfg<256, BN, WN>::NT), 0, s, a);
+  hipLaunchKernelGGL((gg_v3_kernel<BN, WN, NBUF, DIST, QM, OPT>), dim3(grid), dim3(V3Cfg<256, BN, WN>::NT), 0, s, a);
 }
-template <int BN, int WN, int NBUF, int DIST>
+template <int BN, int WN, int NBUF, int DIST, int OPT = 0>
 void launch_v3(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 7) {
-    case 1: launch_v3_q<BN, WN, NBUF, DIST, 1>(a, grid, s); break;
-    case 2: launch_v3_q<BN, WN, NBUF, DIST, 2>(a, grid, s); break;
-    case 4: launch_v3_q<BN, WN, NBUF, DIST, 4>(a, grid, s); break;
-    case 6: launch_v3_q<BN, WN, NBUF, DIST, 6>(a, grid, s); break;
-    default: launch_v3_q<BN, WN, NBUF, DIST, 7>(a, grid, s); break;
+    case 1: launch_v3_q<BN, WN, NBUF, DIST, 1, OPT>(a, grid, s); break;
+    case 2: launch_v3_q<BN, WN, NBUF, DIST, 2, OPT>(a, grid, s); break;
+    case 4: launch_v3_q<BN, WN, NBUF, DIST, 4, OPT>(a, grid, s); break;
+    case 6: launch_v3_q<BN, WN, NBUF, DIST, 6, OPT>(a, grid, s); break;
+    default: launch_v3_q<BN, WN, NBUF, DIST, 7, OPT>(a, grid, s); break;
   }
 }
 
@@ -211,7 +211,7 @@ Variant make_v0(const char* name) {
   return v;
 }
 
-template <int BN, int WN, int NBUF, int DIST>
+template <int BN, int WN, int NBUF, int DIST, int OPT = 0>
 Variant make_v3(const char* name) {
   typedef V3Cfg<256, BN, WN, NBUF, DIST> CT;
   Variant v;
@@ -224,7 +224,7 @@ Variant make_v3(const char* name) {
   v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
   v.k_stage_bytes = 0;
   v.tail_bm = 128;
-  v.launch = &launch_v3<BN, WN, NBUF, DIST>;
+  v.launch = &launch_v3<BN, WN, NBUF, DIST, OPT>;
   return v;
 }
 
@@ -319,6 +319,8 @@ const std::vector<Variant>& variants() {
       make_v2<kV2x | WO_PIPE | WO_STAG>("x_v2x_wo"),
       make_wo2("x_wo2_64"),
       make_wo2<0, 3>("x_wo3_64"),
+      make_v3<128, 2, 3, 2>("x_v3_256x128_2wg"),
+      make_v3<128, 2, 3, 2, 1>("x_v3x_256x128_2wg_buf_spread"),
 #else
       make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
       make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),

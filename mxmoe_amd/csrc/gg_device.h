@@ -1645,6 +1645,14 @@ struct V3Cfg {
   static_assert(DIST < NBUF && DIST <= 4, "ring: stage s+DIST reuses the buffer of stage s-1 at most");
 };
 
+// buffer-form LDS-DMA of one 16-B chunk per lane (v3x): resource `rs`, lane offset `vo`, stage offset `so`
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t v3_rsrc(const uint8_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void v3_bdma(__amdgpu_buffer_rsrc_t rs, uint8_t* dst, uint32_t vo, int so) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)dst, 16, vo, so, 0, 0);
+}
+
 __device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }  // T = {0,2,3,1}
 
 
@@ -1697,7 +1705,10 @@ __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>:
   }
 }
 
-template <class Cfg, int QT>
+// OPT (v3x, lab): 1 = buffer-form LDS-DMA (per-tile buffer resources, fixed 32-bit lane offsets,
+// the stage's K offset in soffset; K-tail chunks past num_records read as zeros) issued one piece
+// per k MFMAs through the steady-state stage (sched_group_barrier), as v2x does for v2
+template <class Cfg, int QT, int OPT = 0>
 __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
                                            const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
@@ -1802,6 +1813,69 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
     }
   };
 
+  if constexpr ((OPT & 1) != 0) {
+    const __amdgpu_buffer_rsrc_t rsA = v3_rsrc(A + (int64_t)m0 * lda);
+    const __amdgpu_buffer_rsrc_t rsB = v3_rsrc(B + (int64_t)n0 * ldb);
+    uint32_t voA[GA], voB[GB];
+    {
+      const int rsub = lane >> 2;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        const int row = (wave * GA + j) * 16 + rsub;
+        voA[j] = (uint32_t)((min(m0 + row, M - 1) - m0) * lda) + kcA[j];
+      }
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const int row = (wave * GB + j) * 16 + rsub;
+        voB[j] = (uint32_t)((min(n0 + row, N - 1) - n0) * ldb) + kcB[j];
+      }
+    }
+    auto bissue = [&](int s, bool full) {
+      uint8_t* As = lds + (s % Cfg::NBUF) * Cfg::STAGE_BYTES;
+      uint8_t* Bs = As + Cfg::A_BYTES;
+      const int kb = s * Cfg::BKB;
+#pragma unroll
+      for (int j = 0; j < GA; ++j)
+        v3_bdma(rsA, As + (wave * GA + j) * 1024, full || kb + kcA[j] < kbytes ? voA[j] : 0x80000000u, kb);
+#pragma unroll
+      for (int j = 0; j < GB; ++j)
+        v3_bdma(rsB, Bs + (wave * GB + j) * 1024, full || kb + kcB[j] < kbytes ? voB[j] : 0x80000000u, kb);
+    };
+    const int nfull = (nst * Cfg::BKB > kbytes) ? nst - 1 : nst;  // stages [0, nfull) have no K tail
+#pragma unroll
+    for (int p = 0; p < Cfg::DIST; ++p)
+      if (p < nst) bissue(p, p < nfull);
+    constexpr int NM = (QT == QT_I4 ? 2 : 1) * FM * FN;  // MFMAs per stage
+    constexpr int KS = NM / DPS > 0 ? NM / DPS : 1;
+    int s = 0;
+    // steady state: stage s + DIST is full and exists; one basic block per stage
+    for (; s + Cfg::DIST < nfull; ++s) {
+      wait_vmcnt<(Cfg::DIST - 1) * DPS>();
+      lds_barrier();
+      bissue(s + Cfg::DIST, true);
+      compute(s);
+#pragma unroll
+      for (int q = 0; q < DPS; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    }
+    for (; s < nst; ++s) {
+      const int later = min(Cfg::DIST - 1, nst - 1 - s);
+      if (later >= 3) wait_vmcnt<(Cfg::DIST >= 4 ? 3 : 2) * DPS>();
+      else if (later == 2) wait_vmcnt<2 * DPS>();
+      else if (later == 1) wait_vmcnt<DPS>();
+      else wait_vmcnt<0>();
+      lds_barrier();
+      if (s + Cfg::DIST < nst) bissue(s + Cfg::DIST, s + Cfg::DIST < nfull);
+      compute(s);
+    }
+    wait_vmcnt<0>();
+    lds_barrier();  // ring -> epilogue staging
+    epilogue_v3<Cfg, QT>(mt, acc, SA, SB, C, m0, n0, lds);
+    return;
+  }
+
   // ---- mainloop: 4-deep ring, 3 stages in flight ----
 #pragma unroll
   for (int p = 0; p < Cfg::DIST; ++p)
@@ -1824,7 +1898,7 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
 
 // QM = set of quant types compiled in (bit 1 << QType, chosen by the plan): a single-type launch
 // carries one tile body, not three
-template <int BN, int WN, int NBUF, int DIST, int QM>
+template <int BN, int WN, int NBUF, int DIST, int QM, int OPT = 0>
 __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2 waves/SIMD: <= 256 VGPRs
   typedef V3Cfg<256, BN, WN, NBUF, DIST> CT;
   typedef V3Cfg<128, BN, WN, NBUF, DIST> CS;
@@ -1839,14 +1913,14 @@ __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2
   _Float16* C = static_cast<_Float16*>(args.ptr_C[td.prob]);
   const bool tall = td.cls == 0;
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
-    if (tall) gg_tile_v3<CT, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v3<CS, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v3<CT, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<CS, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
-    if (tall) gg_tile_v3<CT, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v3<CS, QT_I4>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v3<CT, QT_I4, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<CS, QT_I4, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
-    if (tall) gg_tile_v3<CT, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
-    else gg_tile_v3<CS, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    if (tall) gg_tile_v3<CT, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
+    else gg_tile_v3<CS, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds);
   }
 }
 
