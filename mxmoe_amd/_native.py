@@ -187,12 +187,18 @@ def variant_count() -> int:
     return lib().mxmoe_gg_variant_count()
 
 
-def production_variants(qcfg: str | None = "fp16") -> list[int]:
+GENERAL_QCFGS = ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym")
+
+
+def production_variants(qcfg: str | None = "general") -> list[int]:
     """Compiled variants that compute correct results (``abl_*`` are timing ablations) and have a tile
-    body for ``qcfg`` (default fp16: the general-purpose kernels; ``None``: every one, including the
-    weight-only-only ``wo3_*``)."""
+    body for ``qcfg`` (default "general": fp16, w8a8 and w4a4 — the general-purpose kernels; ``None``:
+    every one, including the small-batch ``wo3_*`` kernel, which has no int4 body)."""
     vs = [int(ln.split()[0]) for ln in list_variants() if not ln.split()[1].startswith("abl_")]
-    return vs if qcfg is None else [v for v in vs if variant_supports(v, qcfg)]
+    if qcfg is None:
+        return vs
+    need = GENERAL_QCFGS if qcfg == "general" else (qcfg,)
+    return [v for v in vs if all(variant_supports(v, q) for q in need)]
 
 
 def plan_tiles(problems, variant: int):

@@ -186,10 +186,12 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
     case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;    // w4a16 only
     case 64: launch_wo2_q<ABL, 64, NWG>(a, grid, s); break;  // w2a16 only
     case 10: launch_wo2_q<ABL, 10, NWG>(a, grid, s); break;  // w4a16 + w8a8 (hz_fused pairing)
+    case 1: launch_wo2_q<ABL, 1, NWG>(a, grid, s); break;    // fp16 only
+    case 2: launch_wo2_q<ABL, 2, NWG>(a, grid, s); break;    // w8a8 only
     // the 8-bit body does not fit 80 VGPRs (3 workgroups per CU) without spilling: calls with w8a16
     // problems run the 2-WG/CU build of the same tiles (same plan: placement only assumes more slots)
     case 16: launch_wo2_q<ABL, 16, 2>(a, grid, s); break;  // w8a16 only
-    default: launch_wo2_q<ABL, 90, 2>(a, grid, s); break;  // any mix of weight-only and w8a8
+    default: launch_wo2_q<ABL, 91, 2>(a, grid, s); break;  // any mix of fp16, w8a8 and weight-only
   }
 }
 
@@ -258,7 +260,8 @@ Variant make_wo2(const char* name) {
   for (int q = 0; q < QT_COUNT; ++q)
     if (!is_weightonly(q)) v.geom[q] = {0, 0, 0, 0};
     else v.geom[q].bm = 64;
-  v.geom[QT_I8] = {64, 128, 128, 512};  // w8a8 beside weight-only problems: 64 x 128 int8 tiles
+  v.geom[QT_I8] = {64, 128, 128, 512};  // w8a8 (beside weight-only problems): 64 x 128 int8 tiles
+  v.geom[QT_F16] = {64, 128, 128, 512};  // fp16: 64 x 128 tiles (64-K stages)
   v.lds_bytes = wo2_lds_bytes<NWG>();
   v.chunk = 32 * NWG;  // NWG workgroups per CU, 32 CUs per XCD
   v.tail_bm = 0;
@@ -374,6 +377,10 @@ constexpr const char* kWoSmallVariant = "wo3_64x256_w8_3wg";
 // the weight-bytes-weighted mean M over the call's problems (qwen2_moe layer 11: ~60 at bs = 128,
 // ~250 at bs = 2048, ~1030 at bs = 8192, where v2x's 256-row tiles are as fast or faster)
 constexpr double kWoSmallMeanRows = 512.0;
+// calls of fp16 / w8a8 problems only (no weight-only one) take wo3 below this mean M: its 64 x 128
+// fp16 / int8 tiles at 3 WG/CU beat v2x at bs 128 / 512 (w8a8 +4-27 %, fp16 -4 .. +14 % per call,
+// +3 % per step) and lose from bs 2048 (mean M ~250) on (profiles/r03/wo2/wo3_fp16_w8a8.jsonl)
+constexpr double kSmallMeanRows = 128.0;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
@@ -1013,8 +1020,10 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   }
   *out = variant_index(kDefaultVariantName);
   const int wo_mask = (1 << QT_W4A16) | (1 << QT_W8A16) | (1 << QT_W2A16);
-  if ((mask & wo_mask) != 0 && (mask & ~(wo_mask | (1 << QT_I8))) == 0) {
-    // (w8a8 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
+  const int small_mask = wo_mask | (1 << QT_I8) | (1 << QT_F16);
+  if (mask != 0 && (mask & ~small_mask) == 0) {
+    // (w8a8 / fp16 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
+    const double limit = (mask & wo_mask) ? kWoSmallMeanRows : kSmallMeanRows;
     // weight-only: the 3-WG/CU 64-row kernel while the rows per weight byte are few (small batches:
     // the 64-row tile is bound by its instruction stream and barriers, a second and third resident
     // workgroup fill each other's waits — +15-70 % on the qwen2_moe calls at bs 128-2048,
@@ -1026,7 +1035,7 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
       wsum += w;
       msum += w * p.M;
     }
-    if (wsum > 0 && msum / wsum <= kWoSmallMeanRows) {
+    if (wsum > 0 && msum / wsum <= limit) {
       const int wi = variant_index(kWoSmallVariant);
       if (!strcmp(variants()[wi].name, kWoSmallVariant)) *out = wi;
     }

@@ -98,18 +98,42 @@ def test_auto_variant_is_v2x_at_every_k():
         assert auto([_prob(M=4096, N=4096, K=K)]) == nat.default_variant()
     from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
 
-    for bs in (8192, 512):
+    for bs in (8192, 2048):
         layer = load_workload(qwen2_layer11_workload(bs))["layer-11"]
         for gg in ("gate_up", "down"):
             probs = [_prob(M=s.M, N=s.N, K=s.K, **f16) for s in layer[gg]]
             assert auto(probs) == nat.default_variant(), (bs, gg)
 
 
+def test_auto_variant_small_batch_fp16_w8a8_runs_wo3():
+    """AUTO (round 3): fp16 / w8a8 calls without weight-only problems take wo3 (64 x 128 tiles, 3 WG
+    per CU) while the weight-bytes-weighted mean M is <= 128 rows (qwen2_moe layer 11 at bs 128 / 512),
+    v2x from bs 2048 on; any int4 problem keeps the general kernels."""
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    wo3 = names.index("wo3_64x256_w8_3wg")
+
+    def auto(ps):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.resolve_variant(arr, len(ps))
+
+    from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
+
+    f16 = dict(a_bits=16, w_bits=16, scale_a=0, scale_b=0)
+    for kw, qstr in ((f16, "fp16"), ({}, "w8a8_g-1_sym")):
+        for bs, want in ((128, wo3), (512, wo3), (2048, nat.default_variant()), (8192, nat.default_variant())):
+            layer = load_workload(qwen2_layer11_workload(bs, **({} if qstr == "fp16" else {"qstr": qstr})))["layer-11"]
+            for gg in ("gate_up", "down"):
+                probs = [_prob(M=s.M, N=s.N, K=s.K, **kw) for s in layer[gg]]
+                assert auto(probs) == want, (qstr, bs, gg)
+                w4 = _prob(M=8, N=256, K=layer[gg][0].K, a_bits=4, w_bits=4)
+                assert auto(probs + [w4]) != wo3, (qstr, bs, gg)
+
+
 def test_auto_variant_weightonly_small_batch_runs_wo3():
     """AUTO (round 3): a call of weight-only problems (w8a8 problems may ride along: the reference's
     small-batch w4a16 + w8a8 pairing) runs wo3 (64-row tiles, 3 workgroups per CU) while the
-    weight-bytes-weighted mean M is <= 512 rows, v2x above; fp16 / w4a4 problems in the call, or no
-    weight-only problem at all, keep v2x (wo3 has no fp16 / int4 tile body)."""
+    weight-bytes-weighted mean M is <= 512 rows, v2x above; int4 problems in the call keep the
+    general kernels (wo3 has no int4 tile body)."""
     names = [ln.split()[1] for ln in nat.list_variants()]
     wo3 = names.index("wo3_64x256_w8_3wg")
 
@@ -130,11 +154,12 @@ def test_auto_variant_weightonly_small_batch_runs_wo3():
                 K = layer[gg][0].K
                 assert auto(probs + [_prob(M=64, N=256, K=K)]) == want, (qstr, bs, gg)  # + a w8a8 problem
                 f16 = _prob(M=64, N=256, K=K, a_bits=16, w_bits=16, scale_a=0, scale_b=0)
-                assert auto(probs + [f16]) == nat.default_variant(), (qstr, bs, gg)
+                assert auto(probs + [f16]) == want, (qstr, bs, gg)  # fp16 rides along too
                 assert auto(probs + [_prob(M=64, N=256, K=K, a_bits=4, w_bits=4)]) == nat.default_variant()
-    assert auto([_prob(M=64, N=256, K=1024)]) == nat.default_variant()  # w8a8 alone: v2x
-    assert not nat.variant_supports(wo3, "fp16") and not nat.variant_supports(wo3, "w4a4_g-1_sym")
-    assert nat.variant_supports(wo3, "w8a8_g-1_sym")
+    assert auto([_prob(M=4096, N=256, K=1024)]) == nat.default_variant()  # w8a8 alone, large M: v2x
+    assert not nat.variant_supports(wo3, "w4a4_g-1_sym") and not nat.variant_supports(wo3, "bf16")
+    assert nat.variant_supports(wo3, "w8a8_g-1_sym") and nat.variant_supports(wo3, "fp16")
+    assert wo3 not in nat.production_variants()  # no int4 body: not a general-purpose kernel
     assert wo3 not in nat.production_variants() and wo3 in nat.production_variants("w4a16_g128_asym")
 
 

@@ -85,8 +85,10 @@ def test_every_tile_planned_once(cfg, bs):
     names = [ln.split()[1] for ln in nat.list_variants()]
     for gg in ("gate_up", "down"):
         _, _, v = check_coverage(layer[gg])
-        # (small-batch weight-only calls, w8a8 riding along, plan for the 3-WG/CU kernel)
-        assert (names[v] == "wo3_64x256_w8_3wg") == (cfg in ("w4a16", "w4a16_w8a8", "w2a16", "w8a16") and bs < 8192)
+        # (small-batch weight-only calls, w8a8 riding along, and fp16 / w8a8 calls at bs <= 512 plan
+        # for the 3-WG/CU kernel)
+        small = (cfg in ("w4a16", "w4a16_w8a8", "w2a16", "w8a16") and bs < 8192) or (cfg in ("fp16", "w8a8") and bs <= 512)
+        assert (names[v] == "wo3_64x256_w8_3wg") == small, (cfg, bs, gg)
 
 
 def test_other_models_and_every_v2_variant():

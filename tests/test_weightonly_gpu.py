@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 V2 = [int(ln.split()[0]) for ln in nat.list_variants() if ln.split()[1].startswith("v2")]
 # weight-only-only kernels (wo3: 64-row tiles, 3 workgroups per CU)
-WO = [v for v in nat.production_variants("w4a16_g-1_asym") if not nat.variant_supports(v, "fp16")]
+WO = [v for v in nat.production_variants("w4a16_g-1_asym") if not nat.variant_supports(v, "w4a4_g-1_sym")]
 QS = [QParams(16, b, g, s) for b in (2, 4, 8) for g in (-1, 128) for s in (True, False)]
 
 
@@ -100,6 +100,29 @@ def test_wo3_w8a8_beside_weightonly_bit_exact(variant):
                 assert (h.result().view(np.uint16) == h.expected().view(np.uint16)).all(), (h.M, h.N, h.K)
         hps = [HostProblem(40, 1024, 8192, W8A8, seed=120, device=DEV),
                HostProblem(20, 512, 1024, QParams(16, 4, 128, False), seed=121, device=DEV)]
+
+
+@pytest.mark.parametrize("variant", WO)
+def test_wo3_fp16_and_w8a8_calls(variant):
+    """wo3's fp16 and int8 bodies (64 x 128 tiles) on their own (QM = 1 / 2 builds, 3 WG/CU) and
+    mixed with weight-only problems (the QM = 91 2-WG/CU build): edge shapes, K tails, a long-K
+    low-fill split-K call; fp16 within the fp16 tolerance, w8a8 bit-exact."""
+    edge = [(1, 128, 256), (17, 136, 128), (130, 264, 432), (300, 520, 512), (64, 8, 1040), (34, 2816, 2048)]
+    sets = [[(M, N, K, FP16) for M, N, K in edge], [(M, N, K, W8A8) for M, N, K in edge],
+            [(M, N, K, q) for (M, N, K), q in zip(edge, [FP16, W8A8, QParams(16, 4, -1, False), FP16, W8A8,
+                                                           QParams(16, 8, 128, True)])],
+            [(128, 2048, 5632, FP16), (9, 2048, 1408, FP16), (128, 2048, 5632, W8A8)]]
+    for k, specs in enumerate(sets):
+        hps = [HostProblem(M, N, K, q, seed=130 + 10 * k + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
+        gg = GroupGemm([h.problem for h in hps], variant=variant)
+        for _ in range(2):
+            gg.launch()
+            torch.cuda.synchronize()
+            for h in hps:
+                if h.q.is_quant and not h.q.is_weight_only:
+                    assert (h.result().view(np.uint16) == h.expected().view(np.uint16)).all(), (k, h.M, h.N, h.K)
+                else:
+                    assert_f16_close(h.result(), h.expected(), h.K)
 
 
 @pytest.mark.parametrize("variant", [None] + WO)  # None: AUTO (wo3 at these batches)
