@@ -109,7 +109,7 @@ def test_wo3_fp16_and_w8a8_calls(variant):
     low-fill split-K call; fp16 within the fp16 tolerance, w8a8 bit-exact."""
     edge = [(1, 128, 256), (17, 136, 128), (130, 264, 432), (300, 520, 512), (64, 8, 1040), (34, 2816, 2048)]
     sets = [[(M, N, K, FP16) for M, N, K in edge], [(M, N, K, W8A8) for M, N, K in edge],
-            [(M, N, K, q) for (M, N, K), q in zip(edge, [FP16, W8A8, QParams(16, 4, -1, False), FP16, W8A8,
+            [(M, N, K, q) for (M, N, K), q in zip(edge, [FP16, W8A8, FP16, QParams(16, 4, -1, False), W8A8,
                                                            QParams(16, 8, 128, True)])],
             [(128, 2048, 5632, FP16), (9, 2048, 1408, FP16), (128, 2048, 5632, W8A8)]]
     for k, specs in enumerate(sets):
