@@ -188,10 +188,12 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
     case 10: launch_wo2_q<ABL, 10, NWG>(a, grid, s); break;  // w4a16 + w8a8 (hz_fused pairing)
     case 1: launch_wo2_q<ABL, 1, NWG>(a, grid, s); break;    // fp16 only
     case 2: launch_wo2_q<ABL, 2, NWG>(a, grid, s); break;    // w8a8 only
+    case 4: launch_wo2_q<ABL, 4, NWG>(a, grid, s); break;    // w4a4 only
+    case 6: launch_wo2_q<ABL, 6, NWG>(a, grid, s); break;    // w4a4 + w8a8 (LP-1 mixed)
     // the 8-bit body does not fit 80 VGPRs (3 workgroups per CU) without spilling: calls with w8a16
     // problems run the 2-WG/CU build of the same tiles (same plan: placement only assumes more slots)
     case 16: launch_wo2_q<ABL, 16, 2>(a, grid, s); break;  // w8a16 only
-    default: launch_wo2_q<ABL, 91, 2>(a, grid, s); break;  // any mix of fp16, w8a8 and weight-only
+    default: launch_wo2_q<ABL, 95, 2>(a, grid, s); break;  // any mix of fp16, w8a8, w4a4 and weight-only
   }
 }
 
@@ -262,6 +264,7 @@ Variant make_wo2(const char* name) {
     else v.geom[q].bm = 64;
   v.geom[QT_I8] = {64, 128, 128, 512};  // w8a8 (beside weight-only problems): 64 x 128 int8 tiles
   v.geom[QT_F16] = {64, 128, 128, 512};  // fp16: 64 x 128 tiles (64-K stages)
+  v.geom[QT_I4] = {64, 128, 128, 512};   // w4a4: 64 x 128 tiles (256-K stages)
   v.lds_bytes = wo2_lds_bytes<NWG>();
   v.chunk = 32 * NWG;  // NWG workgroups per CU, 32 CUs per XCD
   v.tail_bm = 0;
@@ -377,9 +380,10 @@ constexpr const char* kWoSmallVariant = "wo3_64x256_w8_3wg";
 // the weight-bytes-weighted mean M over the call's problems (qwen2_moe layer 11: ~60 at bs = 128,
 // ~250 at bs = 2048, ~1030 at bs = 8192, where v2x's 256-row tiles are as fast or faster)
 constexpr double kWoSmallMeanRows = 512.0;
-// calls of fp16 / w8a8 problems only (no weight-only one) take wo3 below this mean M: its 64 x 128
-// fp16 / int8 tiles at 3 WG/CU beat v2x at bs 128 / 512 (w8a8 +4-27 %, fp16 -4 .. +14 % per call,
-// +3 % per step) and lose from bs 2048 (mean M ~250) on (profiles/r03/wo2/wo3_fp16_w8a8.jsonl)
+// calls of fp16 / w8a8 / w4a4 problems only (no weight-only one) take wo3 below this mean M: its
+// 64 x 128 tiles at 3 WG/CU beat the general kernels at bs 128 / 512 (w8a8 +4-27 %, fp16 -4 .. +14 %
+// per call, w4a4 / LP-1 mixed +16-63 % except mixed bs 128 down -1.5 % vs v3) and lose from bs 2048
+// (mean M ~250) on (profiles/r03/wo2/wo3_fp16_w8a8.jsonl, wo3_w4a4_mixed.jsonl)
 constexpr double kSmallMeanRows = 128.0;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
@@ -1020,7 +1024,7 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   }
   *out = variant_index(kDefaultVariantName);
   const int wo_mask = (1 << QT_W4A16) | (1 << QT_W8A16) | (1 << QT_W2A16);
-  const int small_mask = wo_mask | (1 << QT_I8) | (1 << QT_F16);
+  const int small_mask = wo_mask | (1 << QT_I8) | (1 << QT_F16) | (1 << QT_I4);
   if (mask != 0 && (mask & ~small_mask) == 0) {
     // (w8a8 / fp16 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
     const double limit = (mask & wo_mask) ? kWoSmallMeanRows : kSmallMeanRows;
@@ -1037,9 +1041,11 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
     }
     if (wsum > 0 && msum / wsum <= limit) {
       const int wi = variant_index(kWoSmallVariant);
-      if (!strcmp(variants()[wi].name, kWoSmallVariant)) *out = wi;
+      if (!strcmp(variants()[wi].name, kWoSmallVariant)) {
+        *out = wi;
+        return MXMOE_GG_OK;
+      }
     }
-    return MXMOE_GG_OK;
   }
   if (mask == (1 << QT_I4)) {
     // int4-only: the 256x128 2-WG/CU kernel, unless the call is low-fill enough for the v2s plan

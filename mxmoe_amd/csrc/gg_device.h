@@ -2445,6 +2445,10 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     // fp16 on the same 64 x 128 tile (two 24-KiB stages of 64 K)
     gg_tile_v2<V2Cfg<64, 128, 4, 2>, QT_F16, 0>(mt, A, B, nullptr, nullptr, C, td.m0, td.n0, lds, sk);
+  } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
+    // w4a4 on the same 64 x 128 tile (two 24-KiB stages of 256 K, nibbles widened to int8 MFMA)
+    const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
+    gg_tile_v2<V2Cfg<64, 128, 4, 2>, QT_I4, 0>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);

@@ -106,9 +106,9 @@ def test_auto_variant_is_v2x_at_every_k():
 
 
 def test_auto_variant_small_batch_fp16_w8a8_runs_wo3():
-    """AUTO (round 3): fp16 / w8a8 calls without weight-only problems take wo3 (64 x 128 tiles, 3 WG
-    per CU) while the weight-bytes-weighted mean M is <= 128 rows (qwen2_moe layer 11 at bs 128 / 512),
-    v2x from bs 2048 on; any int4 problem keeps the general kernels."""
+    """AUTO (round 3): fp16 / w8a8 / w4a4 calls without weight-only problems take wo3 (64 x 128 tiles,
+    3 WG per CU) while the weight-bytes-weighted mean M is <= 128 rows (qwen2_moe layer 11 at bs 128 /
+    512), the general kernels from bs 2048 on; a bf16 / E4M3 / w4a4-g128 problem keeps them too."""
     names = [ln.split()[1] for ln in nat.list_variants()]
     wo3 = names.index("wo3_64x256_w8_3wg")
 
@@ -126,7 +126,14 @@ def test_auto_variant_small_batch_fp16_w8a8_runs_wo3():
                 probs = [_prob(M=s.M, N=s.N, K=s.K, **kw) for s in layer[gg]]
                 assert auto(probs) == want, (qstr, bs, gg)
                 w4 = _prob(M=8, N=256, K=layer[gg][0].K, a_bits=4, w_bits=4)
-                assert auto(probs + [w4]) != wo3, (qstr, bs, gg)
+                assert auto(probs + [w4]) == want, (qstr, bs, gg)  # w4a4 rides along
+                bf = _prob(M=8, N=256, K=layer[gg][0].K, a_bits=16, w_bits=16, scale_a=0, scale_b=0, fmt=nat.FMT_BF16)
+                assert auto(probs + [bf]) == nat.default_variant(), (qstr, bs, gg)  # no bf16 body in wo3
+    for bs, want in ((128, wo3), (512, wo3), (2048, None), (8192, None)):  # int4-only: v3 at large batch
+        layer = load_workload(qwen2_layer11_workload(bs, qstr="w4a4_g-1_sym"))["layer-11"]
+        for gg in ("gate_up", "down"):
+            v = auto([_prob(M=s.M, N=s.N, K=s.K, a_bits=4, w_bits=4) for s in layer[gg]])
+            assert (v == wo3) == (want == wo3), (bs, gg, v)
 
 
 def test_auto_variant_weightonly_small_batch_runs_wo3():
@@ -155,12 +162,13 @@ def test_auto_variant_weightonly_small_batch_runs_wo3():
                 assert auto(probs + [_prob(M=64, N=256, K=K)]) == want, (qstr, bs, gg)  # + a w8a8 problem
                 f16 = _prob(M=64, N=256, K=K, a_bits=16, w_bits=16, scale_a=0, scale_b=0)
                 assert auto(probs + [f16]) == want, (qstr, bs, gg)  # fp16 rides along too
-                assert auto(probs + [_prob(M=64, N=256, K=K, a_bits=4, w_bits=4)]) == nat.default_variant()
+                assert auto(probs + [_prob(M=64, N=256, K=K, a_bits=4, w_bits=4)]) == want  # w4a4 too
+                g128 = _prob(M=64, N=256, K=K, a_bits=4, w_bits=4, gsize=128)
+                assert auto(probs + [g128]) == nat.default_variant()  # no w4a4-g128 body in wo3
     assert auto([_prob(M=4096, N=256, K=1024)]) == nat.default_variant()  # w8a8 alone, large M: v2x
-    assert not nat.variant_supports(wo3, "w4a4_g-1_sym") and not nat.variant_supports(wo3, "bf16")
-    assert nat.variant_supports(wo3, "w8a8_g-1_sym") and nat.variant_supports(wo3, "fp16")
-    assert wo3 not in nat.production_variants()  # no int4 body: not a general-purpose kernel
-    assert wo3 not in nat.production_variants() and wo3 in nat.production_variants("w4a16_g128_asym")
+    assert not nat.variant_supports(wo3, "w4a4_g128_sym") and not nat.variant_supports(wo3, "bf16")
+    assert all(nat.variant_supports(wo3, q) for q in ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym"))
+    assert wo3 in nat.production_variants() and wo3 in nat.production_variants("w4a16_g128_asym")
 
 
 def _plan(problems, ws_bytes=1 << 20):

@@ -87,7 +87,7 @@ def test_every_tile_planned_once(cfg, bs):
         _, _, v = check_coverage(layer[gg])
         # (small-batch weight-only calls, w8a8 riding along, and fp16 / w8a8 calls at bs <= 512 plan
         # for the 3-WG/CU kernel)
-        small = (cfg in ("w4a16", "w4a16_w8a8", "w2a16", "w8a16") and bs < 8192) or (cfg in ("fp16", "w8a8") and bs <= 512)
+        small = (cfg in ("w4a16", "w4a16_w8a8", "w2a16", "w8a16") and bs < 8192) or (cfg in ("fp16", "w8a8", "w4a4", "mixed") and bs <= 512)
         assert (names[v] == "wo3_64x256_w8_3wg") == small, (cfg, bs, gg)
 
 

@@ -103,7 +103,7 @@ def test_weightonly_only_on_v2_variants():
             assert "w4a16=TileConfig(BM=256, BN=256, BK=64" in ln and "w8a16=TileConfig(" in ln
         elif name.startswith("wo3"):  # weight-only-only kernel: 64-row tiles, no fp16 / int bodies
             assert st == nat.MXMOE_GG_ERR_WORKSPACE, (name, err)
-            assert "w4a16=TileConfig(BM=64, BN=256, BK=64" in ln and "w4a4_g-1_sym=" not in ln
+            assert "w4a16=TileConfig(BM=64, BN=256, BK=64" in ln and "w4a4_g128_sym=" not in ln
             assert "w8a8_g-1_sym=TileConfig(BM=64, BN=128" in ln  # int8 problems may ride along
         else:
             assert st == nat.MXMOE_GG_ERR_UNSUPPORTED and "does not implement" in err, name

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 V2 = [int(ln.split()[0]) for ln in nat.list_variants() if ln.split()[1].startswith("v2")]
 # weight-only-only kernels (wo3: 64-row tiles, 3 workgroups per CU)
-WO = [v for v in nat.production_variants("w4a16_g-1_asym") if not nat.variant_supports(v, "w4a4_g-1_sym")]
+WO = [v for v in nat.production_variants("w4a16_g-1_asym") if not nat.variant_supports(v, "w4a4_g128_sym")]
 QS = [QParams(16, b, g, s) for b in (2, 4, 8) for g in (-1, 128) for s in (True, False)]
 
 
