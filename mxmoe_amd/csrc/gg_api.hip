@@ -380,11 +380,15 @@ constexpr const char* kWoSmallVariant = "wo3_64x256_w8_3wg";
 // the weight-bytes-weighted mean M over the call's problems (qwen2_moe layer 11: ~60 at bs = 128,
 // ~250 at bs = 2048, ~1030 at bs = 8192, where v2x's 256-row tiles are as fast or faster)
 constexpr double kWoSmallMeanRows = 512.0;
-// calls of fp16 / w8a8 / w4a4 problems only (no weight-only one) take wo3 below this mean M: its
-// 64 x 128 tiles at 3 WG/CU beat the general kernels at bs 128 / 512 (w8a8 +4-27 %, fp16 -4 .. +14 %
-// per call, w4a4 / LP-1 mixed +16-63 % except mixed bs 128 down -1.5 % vs v3) and lose from bs 2048
-// (mean M ~250) on (profiles/r03/wo2/wo3_fp16_w8a8.jsonl, wo3_w4a4_mixed.jsonl)
-constexpr double kSmallMeanRows = 128.0;
+// calls of fp16 / w8a8 / w4a4 problems only (no weight-only one) take wo3 below a mean M of
+// kSmallMeanRows (kSmallMeanRowsI4 with int4 problems), twice that when the call is K-skewed (its
+// longest K >= 2x the weighted mean K: the qwen2_moe down call, whose shared expert has 4x the
+// routed K — few long tiles the general kernels balance poorly). Measured on qwen2_moe layer 11
+// (mean M ~ bs / 8; profiles/r03/wo2/wo3_fp16_w8a8.jsonl, wo3_w4a4_mixed.jsonl, wo3_mid.jsonl):
+// gate_up wins to bs 512 (fp16 -3.5 .. w4a4 +33 %) and 768 with int4, down calls to bs 1024 (fp16)
+// / 1536 (int4), the general kernels beyond.
+constexpr double kSmallMeanRows = 80.0;
+constexpr double kSmallMeanRowsI4 = 112.0;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
 
 int variant_index(const char* name) {
@@ -1027,7 +1031,18 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   const int small_mask = wo_mask | (1 << QT_I8) | (1 << QT_F16) | (1 << QT_I4);
   if (mask != 0 && (mask & ~small_mask) == 0) {
     // (w8a8 / fp16 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
-    const double limit = (mask & wo_mask) ? kWoSmallMeanRows : kSmallMeanRows;
+    double wsum0 = 0, ksum = 0;
+    int kmax = 0;
+    for (const HostProblem& p : hp) {
+      if (p.M <= 0 || p.N <= 0) continue;
+      const double w = (double)p.N * p.K;
+      wsum0 += w;
+      ksum += w * p.K;
+      kmax = std::max(kmax, p.K);
+    }
+    const bool kskew = wsum0 > 0 && kmax >= 2.0 * ksum / wsum0;
+    const double limit = (mask & wo_mask) ? kWoSmallMeanRows
+                                          : ((mask & (1 << QT_I4)) ? kSmallMeanRowsI4 : kSmallMeanRows) * (kskew ? 2.0 : 1.0);
     // weight-only: the 3-WG/CU 64-row kernel while the rows per weight byte are few (small batches:
     // the 64-row tile is bound by its instruction stream and barriers, a second and third resident
     // workgroup fill each other's waits — +15-70 % on the qwen2_moe calls at bs 128-2048,

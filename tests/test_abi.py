@@ -105,6 +105,29 @@ def test_auto_variant_is_v2x_at_every_k():
             assert auto(probs) == nat.default_variant(), (bs, gg)
 
 
+def test_auto_variant_mid_batch_follows_k_skew():
+    """The small-batch limit doubles for K-skewed calls (longest K >= 2x the weighted mean K): the
+    qwen2_moe down call (shared expert K = 5632 vs 1408 routed) stays on wo3 up to bs 1024 (fp16 /
+    w8a8) and 1536 (with int4), its gate_up call only to bs 512 / 768 (profiles/r03/wo2/wo3_mid.jsonl)."""
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    wo3 = names.index("wo3_64x256_w8_3wg")
+
+    def auto(ps):
+        arr = (nat.GGProblemC * len(ps))(*ps)
+        return nat.resolve_variant(arr, len(ps))
+
+    from mxmoe_amd.workload import load_workload, qwen2_layer11_workload
+
+    f16 = dict(a_bits=16, w_bits=16, scale_a=0, scale_b=0)
+    for kw, qkw, gu_max, dn_max in ((f16, {}, 512, 1024), ({}, {"qstr": "w8a8_g-1_sym"}, 512, 1024),
+                                    (dict(a_bits=4, w_bits=4), {"qstr": "w4a4_g-1_sym"}, 768, 1536)):
+        for bs in (512, 768, 1024, 1536, 2048):
+            layer = load_workload(qwen2_layer11_workload(bs, **qkw))["layer-11"]
+            for gg, lim in (("gate_up", gu_max), ("down", dn_max)):
+                v = auto([_prob(M=s.M, N=s.N, K=s.K, **kw) for s in layer[gg]])
+                assert (v == wo3) == (bs <= lim), (qkw, bs, gg, names[v])
+
+
 def test_auto_variant_small_batch_fp16_w8a8_runs_wo3():
     """AUTO (round 3): fp16 / w8a8 / w4a4 calls without weight-only problems take wo3 (64 x 128 tiles,
     3 WG per CU) while the weight-bytes-weighted mean M is <= 128 rows (qwen2_moe layer 11 at bs 128 /
