@@ -76,6 +76,7 @@ struct Variant {
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
   int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
   bool persistent = false;  // v2p: one workgroup per CU walks a planned tile list
+  int (*lds_of)(int qmask) = nullptr;  // LDS of the build a quant-type set launches (default lds_bytes)
   void (*launch)(const GGArgs&, int grid, int qmask, hipStream_t);  // qmask: 1 << QType present
 };
 
@@ -180,6 +181,11 @@ template <int ABL, int QM, int NWG>
 void launch_wo2_q(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((gg_wo2_kernel<ABL, QM, NWG>), dim3(grid), dim3(512), 0, s, a);
 }
+// quant-type sets launched at the variant's NWG (the rest, with 8-bit weight-only problems, run the
+// 2-WG/CU build): keep in step with the switch below
+constexpr bool wo2_full_nwg(int qm) { return qm == 8 || qm == 64 || qm == 10 || qm == 1 || qm == 2 || qm == 4 || qm == 6; }
+template <int NWG>
+int wo2_launch_lds(int qmask) { return wo2_full_nwg(qmask & 511) ? wo2_lds_bytes<NWG>() : wo2_lds_bytes<2>(); }
 template <int ABL, int NWG>
 void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {
@@ -270,6 +276,7 @@ Variant make_wo2(const char* name) {
   v.tail_bm = 0;
   v.tail2_bm = 0;
   v.launch = &launch_wo2<ABL, NWG>;
+  v.lds_of = &wo2_launch_lds<NWG>;
   return v;
 }
 
@@ -1116,9 +1123,9 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
   info->tile_slots = (int)plan.tiles.size();
   info->reserved = 0;
   info->block = v.threads;
-  info->lds_bytes = v.lds_bytes;
   info->qtype_mask = 0;
   for (const GGMeta& m : plan.meta) info->qtype_mask |= 1 << m.qtype;
+  info->lds_bytes = v.lds_of ? v.lds_of(info->qtype_mask) : v.lds_bytes;
   info->splitk_slabs = plan.slabs;
   info->workspace_bytes = (int64_t)l.total;
   info->workspace = ws;

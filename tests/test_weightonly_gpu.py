@@ -68,6 +68,7 @@ def test_wo3_weightonly_mix_and_split_k(variant):
              (96, 256, 512, QParams(16, 2, 128, False)), (7, 136, 1024, QParams(16, 8, 128, False))]
     hps = [HostProblem(M, N, K, q, seed=90 + i, device=DEV) for i, (M, N, K, q) in enumerate(specs)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)
+    assert gg.info.lds_bytes == 78 * 1024  # 8-bit weight-only problems: the 2-WG/CU build
     gg.launch()
     torch.cuda.synchronize()
     _check(hps)
@@ -76,6 +77,7 @@ def test_wo3_weightonly_mix_and_split_k(variant):
           [HostProblem(9, 2048, 1408, QParams(16, 4, 128, False), seed=96 + i, device=DEV) for i in range(4)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)
     assert gg.info.splitk_slabs > 0, "expected a split-K plan"
+    assert gg.info.lds_bytes == 52 * 1024  # 4-bit only: the 3-WG/CU build
     for _ in range(2):  # counters re-armed between launches
         gg.launch()
         torch.cuda.synchronize()
