@@ -355,6 +355,45 @@ def load_pmc_traffic(cfg: str):
         return None
 
 
+def resolve_launch(gpus: int, env, device_count: int) -> tuple[str, str]:
+    """What `bench.py --gpus N` does in this process: ("run", "") runs the ranks' code here (N = 1, or
+    one rank of a launcher that set WORLD_SIZE = N), ("spawn", "") starts N rank processes through
+    torch.distributed.run as a child, ("error", why) refuses. Decided before any GPU call: counting
+    devices does not initialise the GPU on this image. The one-GPU sharing of several ranks is a gloo
+    rehearsal only (MXMOE_DIST_BACKEND=gloo and MXMOE_DIST_SHARE_GPU=1); under RCCL every rank needs a
+    GPU of its own."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    backend = env.get("MXMOE_DIST_BACKEND", "nccl")
+    share = backend == "gloo" and env.get("MXMOE_DIST_SHARE_GPU", "0") == "1"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            return "error", f"WORLD_SIZE={world} but --gpus {gpus}: n_gpus must equal --gpus"
+        if world > 1 and device_count < world and not share:
+            return "error", (f"{world} ranks but {device_count} visible GPU(s); ranks never share a GPU under "
+                             f"{backend} (set MXMOE_DIST_BACKEND=gloo MXMOE_DIST_SHARE_GPU=1 to rehearse on one GPU)")
+        return "run", ""
+    if gpus == 1:
+        return "run", ""
+    if device_count < gpus and not share:
+        return "error", (f"--gpus {gpus} but {device_count} visible GPU(s) (set MXMOE_DIST_BACKEND=gloo "
+                         f"MXMOE_DIST_SHARE_GPU=1 to rehearse on one GPU)")
+    return "spawn", ""
+
+
+def spawn_ranks(gpus: int, argv: list[str]) -> list[str]:
+    """The torch.distributed.run command that starts `gpus` ranks of this script with the same
+    arguments (run as a child process: this process never touches the GPU, so no exec is needed)."""
+    import socket
+
+    with socket.socket() as s:  # a free port on the loopback rendezvous address
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -376,16 +415,26 @@ def main():
     ap.add_argument("--extras-warmup", type=int, default=200, help="untimed steps before an extra config's launch timing")
     args = ap.parse_args()
 
+    action, why = resolve_launch(args.gpus, os.environ, torch.cuda.device_count())
+    if action == "error":
+        log("bench.py: " + why)
+        sys.exit(2)
+    if action == "spawn":
+        import subprocess
+
+        sys.exit(subprocess.call(spawn_ranks(args.gpus, sys.argv[1:])))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # MXMOE_DIST_BACKEND=gloo rehearses the N > 1 path with several ranks on one GPU (collectives
-    # staged through host memory); the node runs use RCCL ("nccl")
+    # MXMOE_DIST_BACKEND=gloo rehearses the N > 1 path (collectives staged through host memory; with
+    # MXMOE_DIST_SHARE_GPU=1 several ranks may share one GPU); the node runs use RCCL ("nccl")
     backend = os.environ.get("MXMOE_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
 
-        local = local % max(1, torch.cuda.device_count())
+        if local >= torch.cuda.device_count():  # resolve_launch allowed it: the gloo one-GPU rehearsal
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -157,7 +157,10 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
 /* Re-point a plan at new operand buffers: `problems` must describe the same shapes, quant params
  * and strides as the planned call (checked through the plan signature, MXMOE_GG_ERR_INVALID
  * otherwise); only the 5 pointer columns of the workspace are uploaded (one copy on `stream` and a
- * stream synchronisation). The pointers get mxmoe_gg_plan's NULL / alignment checks. */
+ * stream synchronisation). The pointers get mxmoe_gg_plan's NULL / alignment checks.
+ * BLOCKING and NOT graph-capturable (unlike mxmoe_gg_launch): the host re-runs the planner to
+ * form the signature and the call ends with hipStreamSynchronize(stream). A plan must be rebound
+ * on the stream its launches run on: the upload is ordered behind that stream's work only. */
 int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const mxmoe_gg_plan_info* info, void* stream);
 
 /* Launch a planned GroupGEMM on `stream`. No allocation, no synchronisation. */

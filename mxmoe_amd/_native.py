@@ -193,7 +193,8 @@ GENERAL_QCFGS = ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym")
 def production_variants(qcfg: str | None = "general") -> list[int]:
     """Compiled variants that compute correct results (``abl_*`` are timing ablations) and have a tile
     body for ``qcfg`` (default "general": fp16, w8a8 and w4a4 — the general-purpose kernels; ``None``:
-    every one, including the small-batch ``wo3_*`` kernel, which has no int4 body)."""
+    every one). The small-batch ``wo3_*`` kernel has fp16, w8a8, w4a4 and weight-only bodies (not
+    w4a4_g128, E4M3 or bf16), so it is in the "general" set too."""
     vs = [int(ln.split()[0]) for ln in list_variants() if not ln.split()[1].startswith("abl_")]
     if qcfg is None:
         return vs

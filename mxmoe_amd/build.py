@@ -48,5 +48,25 @@ def build(force: bool = False, verbose: bool = False, extra: list[str] | None = 
     return out
 
 
+REF_HARNESS_SRC = [ROOT / "tests" / "cpp" / "ref_harness_call.cpp", ROOT / "tests" / "cpp" / "layout_check.cpp"]
+REF_HARNESS = ROOT / "tests" / "cpp" / "bin" / "ref_harness_call"
+
+
+def build_ref_harness(force: bool = False, verbose: bool = False) -> Path:
+    """The reference-side C++ caller of groupgemm_mxmoe (tests/cpp): test
+    infrastructure, linked against the product library (rpath to mxmoe_amd/lib)."""
+    deps = REF_HARNESS_SRC + [ROOT / "include" / "mxmoe_gg.h", LIB]
+    if not force and REF_HARNESS.exists() and all(p.stat().st_mtime <= REF_HARNESS.stat().st_mtime for p in deps):
+        return REF_HARNESS
+    REF_HARNESS.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-I", str(ROOT / "include"),
+           "-o", str(REF_HARNESS), *map(str, REF_HARNESS_SRC), "-L", str(LIB.parent), "-lmxmoe_gg",
+           "-Wl,-rpath,$ORIGIN/../../../mxmoe_amd/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return REF_HARNESS
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True, lab="--lab" in sys.argv, lab_fast="--lab-fast" in sys.argv))

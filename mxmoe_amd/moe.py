@@ -336,16 +336,36 @@ def gg_mxmoe_share_fused(inp: Sequence[torch.Tensor], experts: Sequence[torch.Te
         raise ValueError(f"gg_mxmoe_share_fused: {len(inp)} inputs for {pi} non-empty experts")
     if not probs:
         return output
-    key = (probs[0].C.device, tuple((p.M, p.N, p.K, p.q) for p in probs))
+    s = stream if stream is not None else torch.cuda.current_stream(probs[0].C.device)
+    # one plan per (device, stream, shapes, qparams, strides): a plan's workspace is only ever rebound
+    # and launched on its own stream, so a rebind (blocking on that stream) never re-points the
+    # operands of a launch still running on another one
+    key = (probs[0].C.device, int(s.cuda_stream), tuple((p.M, p.N, p.K, p.q, p.lda, p.ldb, p.ldc) for p in probs))
     gg = _SHARE_FUSED_PLANS.get(key)
+    if gg is not None:
+        try:
+            gg.rebind(probs, stream=s)
+        except nat.GGError:  # the library's plan signature disagrees (e.g. a stride the key missed): re-plan
+            _evict_share_fused(key)
+            gg = None
     if gg is None:
         if len(_SHARE_FUSED_PLANS) >= 64:
-            _SHARE_FUSED_PLANS.clear()
-        gg = _SHARE_FUSED_PLANS[key] = GroupGemm(probs, stream=stream)
-    else:
-        gg.rebind(probs, stream=stream)
-    gg.launch(stream)
+            for k in list(_SHARE_FUSED_PLANS):
+                _evict_share_fused(k)
+        gg = GroupGemm(probs, stream=s)
+        gg.stream = s
+        if s != torch.cuda.current_stream(gg.device):  # allocated on the current stream, used on s
+            gg.workspace.record_stream(s)
+        _SHARE_FUSED_PLANS[key] = gg
+    gg.launch(s)
     return output
+
+
+def _evict_share_fused(key) -> None:
+    """Drop a cached plan whose launches may still be running on its stream: record the workspace on
+    that stream first, so the caching allocator does not hand the memory out before they finish."""
+    gg = _SHARE_FUSED_PLANS.pop(key)
+    gg.workspace.record_stream(gg.stream)
 
 
 # ------------------------------------------------------------------ the MoE FFN layer

@@ -293,3 +293,40 @@ def test_fast_quotient_matches_ieee_division():
                 q2 = (e.astype(np.float64) * r + q.astype(np.float64)).astype(np.float32)
                 got = np.rint(np.clip(q2.astype(np.float16).astype(np.float32), -127, 127))
                 assert (got == ref).all()
+
+
+@pytest.mark.gpu
+def test_gg_mxmoe_share_fused_streams_and_strided_output(gpu):
+    """The share_fused plan cache keys on the stream and the operand strides: the same
+    shapes launched on two streams get two plans (a rebind on one stream never re-points a launch
+    in flight on the other), and an output written through a strided view (ldc > N) re-plans instead
+    of raising. Both are bit-exact against the oracle."""
+    T, topk, E, H, N = 64, 2, 3, 256, 128
+    g = torch.Generator().manual_seed(31)
+    qs = [W8A8, W4A4, W8A8, W8A8]
+    qparams = [(q.a_bits, q.w_bits, q.gsize, q.sym) for q in qs]
+    ws = [moe.prepare_weight((((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half()).to(DEV), q) for q in qs]
+    ids = _ids(T, topk, E, 32)
+    moe._SHARE_FUSED_PLANS.clear()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    h = _hidden(T, H, 33).to(DEV)
+    inp, sc, out, *_rest = moe.quant_inp_act(h, ids.to(DEV), E, N, 1, qparams)
+    counts = _rest[3]
+    torch.cuda.synchronize()
+    wide = [torch.zeros(o.shape[0], 2 * N + 64, dtype=torch.float16, device=DEV) for o in out]
+    outs = {"s1": [torch.empty_like(o) for o in out], "s2": [torch.empty_like(o) for o in out],
+            "strided": [w[:, 16:16 + 2 * N] for w in wide]}
+    for name, st in (("s1", s1), ("s2", s2), ("strided", s1)):
+        moe.gg_mxmoe_share_fused(inp, [w.B for w in ws], sc, [w.scale_b for w in ws], outs[name], 2 * N, H, 2 * N, H,
+                                 qparams, counts, stream=st)
+    torch.cuda.synchronize()
+    assert len(moe._SHARE_FUSED_PLANS) == 3  # s1, s2 and the strided s1 plan
+    experts = [e for e in range(E) if int(counts[e]) > 0] + [E]
+    for pi, e in enumerate(experts):
+        w = ws[e]
+        A, sa = inp[pi].cpu().numpy(), sc[pi].cpu().numpy()
+        ref = oracle.gg_quant(A, w.B.cpu().numpy(), sa, w.scale_b.cpu().numpy(), A.shape[0], w.N, w.K, w.q.a_bits)
+        for name in outs:
+            got = outs[name][pi].cpu().numpy()
+            assert (got.view(np.uint16) == ref.view(np.uint16)).all(), f"{name} expert {e}"
+        assert (wide[pi][:, :16] == 0).all() and (wide[pi][:, 16 + 2 * N:] == 0).all()  # nothing outside the view

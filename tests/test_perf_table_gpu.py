@@ -49,7 +49,10 @@ def test_cost_model_predicts_layer_calls():
         pred = {c: res[(c, g)][0] for c in ("fp16", "w8a8", "w4a4")}
         meas = {c: res[(c, g)][1] for c in ("fp16", "w8a8", "w4a4")}
         assert max(pred, key=pred.get) == max(meas, key=meas.get) == "fp16", (g, pred, meas)
-        # w8a8 (v2x) and w4a4 (v3) run within a few % of each other since round 3; the order of a
-        # pair closer than 5 % in either column is noise, a wider gap must be ranked the same way
-        if abs(meas["w8a8"] / meas["w4a4"] - 1) > 0.05 and abs(pred["w8a8"] / pred["w4a4"] - 1) > 0.05:
+        # w8a8 (v2x) and w4a4 (v3) run within a few % of each other since round 3: a measured gap
+        # under 5 % is a tie, which the model must then also predict as close (< 10 %); a wider
+        # measured gap must be ranked the same way
+        if abs(meas["w8a8"] / meas["w4a4"] - 1) <= 0.05:
+            assert abs(pred["w8a8"] / pred["w4a4"] - 1) < 0.10, (g, pred, meas)
+        else:
             assert (pred["w8a8"] < pred["w4a4"]) == (meas["w8a8"] < meas["w4a4"]), (g, pred, meas)

@@ -3,6 +3,9 @@
 set -o pipefail
 TAG=${1:-region2}
 cd $GRAFT_REPO_ROOT
+# the planner A/B switches (MXMOE_GG_BAND / _REGION / ...) exist only in the lab library (-DMXMOE_LAB)
+export MXMOE_GG_LIB=$PWD/mxmoe_amd/lib/libmxmoe_gg_lab.so
+[ -f "$MXMOE_GG_LIB" ] || { echo "build the lab library first: python -m mxmoe_amd.build --lab"; exit 1; }
 mkdir -p gpurun_out/$TAG
 V="auto,auto@MXMOE_GG_REGION=0,auto@MXMOE_GG_REGION=2,auto@MXMOE_GG_ALIGN=0"
 for cg in "fp16 gate_up" "fp16 down" "w8a8 gate_up" "w8a8 down" "mixed gate_up"; do
