@@ -17,7 +17,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MXMOE_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [CSRC / "gg_api.hip", CSRC / "moe_ops.hip"]
-DEPS = SOURCES + [CSRC / "gg_device.h", ROOT / "include" / "mxmoe_gg.h", ROOT / "include" / "mxmoe_moe.h"]
+DEPS = SOURCES + [CSRC / "gg_device.h", CSRC / "gg_v2q.h", ROOT / "include" / "mxmoe_gg.h", ROOT / "include" / "mxmoe_moe.h"]
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", str(ROOT / "include")]

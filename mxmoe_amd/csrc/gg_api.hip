@@ -24,6 +24,7 @@
 
 #include "../../include/mxmoe_gg.h"
 #include "gg_device.h"
+#include "gg_v2q.h"
 
 using namespace mxmoe;
 
@@ -177,6 +178,28 @@ void launch_v2p(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   }
 }
 
+template <int QM, int TRACE>
+void launch_v2q_q(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gg_v2q_kernel<QM, TRACE>), dim3(grid), dim3(512), 0, s, a);
+}
+template <int TRACE = 0>
+void launch_v2q(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  switch (qmask & 511) {
+    case 1: launch_v2q_q<1, TRACE>(a, grid, s); break;
+    case 2: launch_v2q_q<2, TRACE>(a, grid, s); break;
+#ifndef MXMOE_LAB_FAST
+    case 4: launch_v2q_q<4, TRACE>(a, grid, s); break;
+    case 6: launch_v2q_q<6, TRACE>(a, grid, s); break;
+    case 256: launch_v2q_q<256, TRACE>(a, grid, s); break;
+    default: launch_v2q_q<511, TRACE>(a, grid, s); break;  // every tile body
+#else
+    default:
+      fprintf(stderr, "libmxmoe_gg_lab (fast): v2q quant-type mix %#x not compiled\n", qmask);
+      abort();
+#endif
+  }
+}
+
 template <int ABL, int QM, int NWG>
 void launch_wo2_q(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((gg_wo2_kernel<ABL, QM, NWG>), dim3(grid), dim3(512), 0, s, a);
@@ -289,6 +312,15 @@ Variant make_v2p(const char* name) {
   return v;
 }
 
+// v2q: the persistent v2x with the register epilogue and the next tile's ring fill before it
+// (gg_v2q.h); planned like v2p (per-workgroup tile lists)
+template <int TRACE = 0>
+Variant make_v2q(const char* name) {
+  Variant v = make_v2p<0>(name);
+  v.launch = &launch_v2q<TRACE>;
+  return v;
+}
+
 // the round-3 AUTO default's mainloop flags (variant v2x_256x256_w8_b3_buf_spread_edma, without the
 // weight-only options)
 constexpr int kV2x = V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT);
@@ -304,15 +336,9 @@ typedef TileCfg<128, 256, 2, 2, 1> T128x256;
 const std::vector<Variant>& variants() {
   static const std::vector<Variant> v = {
 #ifndef MXMOE_LAB
-      make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
-      make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
-      make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
-      make_v2("v2_256x256_w8_dma"),
-      make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
+      // round 4: the product lists what AUTO picks; the round-1/2 kernels (v0
+      // register-staged tiles, plain / staggered v2, v3 256 x 256) live on in the lab build
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
-      make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
-      // staggered v2 with B two stages ahead (3-stage B ring, 160 KiB)
-      make_v2<V2_STAGGER | V2_B3>("v2s3_256x256_w8_dma_stagger_bring3"),
       // round 3 (AUTO default): v2s3's LDS image, buffer-form LDS-DMA spread over the first MFMA
       // group of each half stage, issued by waves 0-3 for their SIMD partners too (not on int4
       // tiles) — profiles/r03/lab/
@@ -326,15 +352,17 @@ const std::vector<Variant>& variants() {
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
       // experiments under test only, fp16 / w8a8 bodies only
       make_v2<kV2x>("x_v2x"),
-      make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
-      make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
-      make_v2<kV2x | V2_EPIPE | V2_LATEIL>("x_v2x_epipe_lateil"),
-      make_v2<kV2x | WO_PIPE | WO_STAG>("x_v2x_wo"),
-      make_wo2("x_wo2_64"),
-      make_wo2<0, 3>("x_wo3_64"),
-      make_v3<128, 2, 3, 2>("x_v3_256x128_2wg"),
-      make_v3<128, 2, 3, 2, 1>("x_v3x_256x128_2wg_buf_spread"),
+      make_v2<kV2x | V2_DIRECT>("x_v2x_direct"),
+      make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),
+      make_v2<kV2x | V2_DIRECT | V2_TRACE>("abl_v2x_direct_trace"),
+      make_v2q("x_v2q"),
+      make_v2q<1>("abl_v2q_trace"),
 #else
+      make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
+      make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
+      make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
+      make_v2("v2_256x256_w8_dma"),
+      make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
       make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
       make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),

@@ -166,10 +166,10 @@ def test_nslice_views_match_full_call():
                 assert torch.equal(p.C.view(torch.int16), r.view(torch.int16)), (world, i)
 
 
-B3 = [ln.split()[1] for ln in nat.list_variants()].index("v2s3_256x256_w8_dma_stagger_bring3")
+B3 = [ln.split()[1] for ln in nat.list_variants()].index("v2x_256x256_w8_b3_buf_spread_edma")
 
 
-@pytest.mark.parametrize("variant", [None, B3], ids=["auto", "v2s3"])
+@pytest.mark.parametrize("variant", [None, B3], ids=["auto", "v2x"])
 @pytest.mark.parametrize("q", [FP16, W8A8, W4A4, QParams(16, 4, 128, False)], ids=["fp16", "w8a8", "w4a4", "w4a16g128"])
 def test_splitk_long_k_low_fill(q, variant):
     """Low-fill calls with a long K (the shared expert's down at small batch) are split along K;

@@ -301,9 +301,9 @@ def test_gg_mxmoe_share_fused_streams_and_strided_output(gpu):
     shapes launched on two streams get two plans (a rebind on one stream never re-points a launch
     in flight on the other), and an output written through a strided view (ldc > N) re-plans instead
     of raising. Both are bit-exact against the oracle."""
-    T, topk, E, H, N = 64, 2, 3, 256, 128
+    T, topk, E, H, N = 64, 2, 5, 256, 128  # (_ids leaves expert 3 empty)
     g = torch.Generator().manual_seed(31)
-    qs = [W8A8, W4A4, W8A8, W8A8]
+    qs = [W8A8, W4A4, W8A8, W4A4, W8A8, W8A8]
     qparams = [(q.a_bits, q.w_bits, q.gsize, q.sym) for q in qs]
     ws = [moe.prepare_weight((((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half()).to(DEV), q) for q in qs]
     ids = _ids(T, topk, E, 32)
