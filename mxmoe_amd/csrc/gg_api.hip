@@ -76,7 +76,9 @@ struct Variant {
   int k_stage_bytes;   // K bytes per row must be a multiple of this (0 = any multiple of 16)
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
   int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
-  bool persistent = false;  // v2p: one workgroup per CU walks a planned tile list
+  bool persistent = false;  // v2p / v2q: a workgroup walks a planned tile list
+  int persist_len = 0;      // v2q: 0 = one list per CU (static); L > 0 = lists of L consecutive XCD-queue
+                            // tiles, one per block, the hardware dispatching blocks as CUs free up
   int (*lds_of)(int qmask) = nullptr;  // LDS of the build a quant-type set launches (default lds_bytes)
   void (*launch)(const GGArgs&, int grid, int qmask, hipStream_t);  // qmask: 1 << QType present
 };
@@ -315,9 +317,10 @@ Variant make_v2p(const char* name) {
 // v2q: the persistent v2x with the register epilogue and the next tile's ring fill before it
 // (gg_v2q.h); planned like v2p (per-workgroup tile lists)
 template <int TRACE = 0>
-Variant make_v2q(const char* name) {
+Variant make_v2q(const char* name, int persist_len = 0) {
   Variant v = make_v2p<0>(name);
   v.launch = &launch_v2q<TRACE>;
+  v.persist_len = persist_len;
   return v;
 }
 
@@ -357,6 +360,9 @@ const std::vector<Variant>& variants() {
       make_v2<kV2x | V2_DIRECT | V2_TRACE>("abl_v2x_direct_trace"),
       make_v2q("x_v2q"),
       make_v2q<1>("abl_v2q_trace"),
+      make_v2q("x_v2q_l2", 2),
+      make_v2q("x_v2q_l4", 4),
+      make_v2q<1>("abl_v2q_l2_trace", 2),
 #else
       make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
       make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
@@ -1015,7 +1021,22 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   }
 #endif
   plan->launch_grid = grid;
-  if (v.persistent) {
+  if (v.persistent && v.persist_len > 0) {
+    // v2q with block lists: XCD x's queue cut into groups of L consecutive tiles, group g run by
+    // block 8 g + x (that XCD under round-robin placement: speed only); the hardware hands a freed
+    // CU the next block, as for the one-tile blocks. Table [k][G] with a terminating row.
+    const int L = v.persist_len;
+    size_t ngroups = 0;
+    for (const auto& q : queue) ngroups = std::max(ngroups, (q.size() + L - 1) / L);
+    const int G = (int)(8 * ngroups);
+    plan->tiles.assign((size_t)(L + 1) * G, TileDesc{-1, 0, 0, 0, 0, 0, -1, -1});
+    for (int x = 0; x < 8; ++x)
+      for (size_t j = 0; j < queue[x].size(); ++j) {
+        const size_t g = j / L, k = j % L;
+        plan->tiles[k * G + 8 * g + x] = all_tiles[queue[x][j]];
+      }
+    plan->launch_grid = T > 0 ? G : 0;
+  } else if (v.persistent) {
     // v2p: each XCD's queue handed out to its `chunk` workgroups in queue order, every tile to the
     // workgroup whose modelled finish is earliest (what the hardware's dispatch does with blocks,
     // planned once here); workgroup w = 8 * slot + x sits on XCD x under round-robin placement

@@ -85,6 +85,20 @@ def build_layer_inputs(shapes: Sequence[QShape], device="cuda", seed: int = 42,
     return LayerInputs(problems=probs, shapes=list(shapes))
 
 
+def refill_layer_inputs(inp: LayerInputs, seed: int = 42) -> None:
+    """Regenerate a call's operands (the same seeded values as build_layer_inputs) in place, so a
+    plan made on the buffers stays valid: operands materialised after planning, as a serving loop
+    plans once per shape and receives data per batch."""
+    dev = inp.problems[0].C.device if inp.problems else torch.device("cuda")
+    fresh = build_layer_inputs(inp.shapes, device=dev, seed=seed)
+    for p, q in zip(inp.problems, fresh.problems):
+        for name in ("A", "B", "scale_a", "scale_b"):
+            dst, src = getattr(p, name), getattr(q, name)
+            if dst is not None:
+                dst.copy_(src)
+    del fresh
+
+
 def time_launches(fn, warmup: int = 20, iters: int = 50, stream: Optional[torch.cuda.Stream] = None) -> dict:
     """Per-call device time with events on the launch stream; median / mean / min in ms."""
     s = stream if stream is not None else torch.cuda.current_stream()
