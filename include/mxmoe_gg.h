@@ -29,7 +29,9 @@
  *     device memory except the reference-compatible shim groupgemm_mxmoe();
  *   - explicit stream argument (hipStream_t passed as void*); mxmoe_gg_launch() does no host
  *     synchronisation and no allocation, so it can be captured into a hipGraph;
- *   - no mutable global state besides the thread-local error string.
+ *   - mutable global state: the thread-local error string, the reference shim's per-device
+ *     workspaces (mxmoe_gg_release_shim_workspaces) and mxmoe_gg_rebind's per-workspace plan keys
+ *     (mutex-guarded, host memory only).
  */
 #ifndef MXMOE_GG_H_
 #define MXMOE_GG_H_
@@ -138,10 +140,9 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
 #define MXMOE_GG_VARIANT_AUTO (-1)
 
 /* The concrete variant `variant` (MXMOE_GG_VARIANT_AUTO or an index) resolves to for these
- * problems, written to *out. Host only (no GPU). AUTO: w4a4-only sets -> the 256x128 2-WG/CU
- * kernel (unless the plan needs split-K); calls whose median tile has <= 24 128-B K stages, or
- * whose tiles are mostly fp16 64-row remainders (small batches) -> the 3-stage-B-ring staggered
- * kernel; otherwise mxmoe_gg_default_variant(). */
+ * problems, written to *out. Host only (no GPU). AUTO: small-batch calls (mean rows per weight
+ * byte under the DESIGN.md §4 cuts) -> the 3-WG/CU 64-row kernel (wo3); w4a4-only sets -> the
+ * 256x128 2-WG/CU kernel (unless the plan needs split-K); otherwise mxmoe_gg_default_variant(). */
 int mxmoe_gg_resolve_variant(const mxmoe_gg_problem* problems, int problem_count, int variant, int* out);
 
 /* Device workspace bytes the plan of these problems needs with this variant
@@ -158,9 +159,11 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
  * and strides as the planned call (checked through the plan signature, MXMOE_GG_ERR_INVALID
  * otherwise); only the 5 pointer columns of the workspace are uploaded (one copy on `stream` and a
  * stream synchronisation). The pointers get mxmoe_gg_plan's NULL / alignment checks.
- * BLOCKING and NOT graph-capturable (unlike mxmoe_gg_launch): the host re-runs the planner to
- * form the signature and the call ends with hipStreamSynchronize(stream). A plan must be rebound
- * on the stream its launches run on: the upload is ordered behind that stream's work only. */
+ * BLOCKING and NOT graph-capturable (unlike mxmoe_gg_launch): the call ends with
+ * hipStreamSynchronize(stream). The library remembers, per workspace, a key over the planned
+ * shapes / quant params / strides: a rebind with the same key skips the host planner (pointers are
+ * still checked); otherwise the planner re-runs to compare the plan signature. A plan must be
+ * rebound on the stream its launches run on: the upload is ordered behind that stream's work only. */
 int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const mxmoe_gg_plan_info* info, void* stream);
 
 /* Launch a planned GroupGEMM on `stream`. No allocation, no synchronisation. */
