@@ -26,6 +26,9 @@ namespace mxmoe {
 
 // LDS map (as v2x with V2_B3): A slots [0, 32K) [32K, 64K); B ring [64K, 96K) [96K, 128K) [128K, 160K)
 constexpr int Q_ASLOT = 32768, Q_BBASE = 65536, Q_BSLOT = 32768;
+// C store cache policy (template SAUX): 16 = sc1 (write-once lines leave the XCD's L2; v2x's
+// choice), 0 = plain. tools/store_probe.hip: a 128-KiB tile drains in 1366 (plain) vs 2434 (sc1)
+// cycles with 32 CUs storing.
 
 // What a tile leaves in flight for the next one (per wave: the counts differ between early and
 // late waves): `pref` the next tile's ring was filled by the previous tile, `after` LDS-DMA pieces
@@ -80,32 +83,46 @@ __device__ __forceinline__ int q_dma(const __amdgpu_buffer_rsrc_t& rs, int G, in
   return n;
 }
 
-// The ring fill of tile `t` (A0, B0, B1, A1, B2 as far as the tile has stages), in that order so
-// that "A0 and B0 landed" is vmcnt(pieces issued after them). Returns {pieces issued in all, pieces
-// issued after A0 / B0} (this wave's).
-__device__ __forceinline__ int2 q_fill(const PTile& t, uint8_t* lds, int wave, int lane) {
+// The ring fill of tile `t`, issued by the early waves for every quant type (each issues its
+// partner's rows too): head = A0, B0, B1, tail = A1, B2 (as far as the tile has stages). In that
+// order "A0 and B0 landed" is vmcnt(pieces issued after them). q_fill_head returns {pieces in
+// all, pieces after A0 / B0}; q_fill_tail the pieces it issued (this wave's counts).
+struct QFillSrc {
+  __amdgpu_buffer_rsrc_t a, b;
+  int GA, nst, kb0;
+};
+__device__ __forceinline__ QFillSrc q_fill_src(const PTile& t) {
   const GGMeta& m = t.mt;
   const int bm = t.cls == 0 ? 256 : t.cls == 1 ? 128 : 64;
-  const int GA = bm / 64, GB = 4;
-  const bool edma = q_edma(m.qtype);
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(t.A) + (int64_t)t.m0 * m.lda_b, (short)0, (int)(min(m.M - t.m0, bm) * m.lda_b), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(t.B) + (int64_t)t.n0 * m.ldb_b, (short)0, (int)(min(m.N - t.n0, 256) * m.ldb_b), 0x00020000);
-  const int nst = t.sk.nst, kb0 = t.sk.ks0 * 128;
-  if (nst <= 0) return int2{0, 0};
-  int first = q_dma(rsA, GA, m.lda_b, kb0, m.kbytes, edma, wave, lane, lds);
-  first += q_dma(rsB, GB, m.ldb_b, kb0, m.kbytes, edma, wave, lane, lds + Q_BBASE);
-  int after = 0;
-  if (nst > 1) {
-    after += q_dma(rsB, GB, m.ldb_b, kb0 + 128, m.kbytes, edma, wave, lane, lds + Q_BBASE + Q_BSLOT);
-    after += q_dma(rsA, GA, m.lda_b, kb0 + 128, m.kbytes, edma, wave, lane, lds + Q_ASLOT);
-  }
-  if (nst > 2) after += q_dma(rsB, GB, m.ldb_b, kb0 + 256, m.kbytes, edma, wave, lane, lds + Q_BBASE + 2 * Q_BSLOT);
+  QFillSrc f;
+  f.a = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(t.A) + (int64_t)t.m0 * m.lda_b, (short)0,
+                                          (int)(min(m.M - t.m0, bm) * m.lda_b), 0x00020000);
+  f.b = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(t.B) + (int64_t)t.n0 * m.ldb_b, (short)0,
+                                          (int)(min(m.N - t.n0, 256) * m.ldb_b), 0x00020000);
+  f.GA = bm / 64;
+  f.nst = t.sk.nst;
+  f.kb0 = t.sk.ks0 * 128;
+  return f;
+}
+__device__ __forceinline__ int2 q_fill_head(const PTile& t, uint8_t* lds, int wave, int lane) {
+  const GGMeta& m = t.mt;
+  const QFillSrc f = q_fill_src(t);
+  if (f.nst <= 0) return int2{0, 0};
+  int first = q_dma(f.a, f.GA, m.lda_b, f.kb0, m.kbytes, true, wave, lane, lds);
+  first += q_dma(f.b, 4, m.ldb_b, f.kb0, m.kbytes, true, wave, lane, lds + Q_BBASE);
+  const int after = f.nst > 1 ? q_dma(f.b, 4, m.ldb_b, f.kb0 + 128, m.kbytes, true, wave, lane, lds + Q_BBASE + Q_BSLOT) : 0;
   return int2{first + after, after};
 }
+__device__ __forceinline__ int q_fill_tail(const PTile& t, uint8_t* lds, int wave, int lane) {
+  const GGMeta& m = t.mt;
+  const QFillSrc f = q_fill_src(t);
+  int n = 0;
+  if (f.nst > 1) n += q_dma(f.a, f.GA, m.lda_b, f.kb0 + 128, m.kbytes, true, wave, lane, lds + Q_ASLOT);
+  if (f.nst > 2) n += q_dma(f.b, 4, m.ldb_b, f.kb0 + 256, m.kbytes, true, wave, lane, lds + Q_BBASE + 2 * Q_BSLOT);
+  return n;
+}
 
-template <class Cfg, int QT, int TRACE = 0>
+template <class Cfg, int QT, int TRACE = 0, int SAUX = 16>
 __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, int nx_idx, QState st, uint8_t* lds) {
   constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
   typedef typename AccT<QT>::type acc_t;
@@ -203,19 +220,21 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
   // ---- prologue: the ring fill (issued by the previous tile when st.pref), A0 / B0 landed ----
   if (nst > 0) {
     if (!st.pref) {
-      st.after = q_fill(t, lds, wave, lane).y;
+      st.after = q_fill_head(t, lds, wave, lane).y + q_fill_tail(t, lds, wave, lane);
       st.stores = 0;
     }
     q_wait_le(st.after + st.stores);
     lds_barrier();
     // iteration 0: A1 / B1 landed; B2 and the previous tile's stores may stay in flight
-    const int w0 = (nst > 2 ? pw * GB : 0) + st.stores;
+    // (early waves: the fill's B2 and this wave's stores of the previous tile may stay in flight;
+    //  the late waves have no loads outstanding: the fill is the early waves')
+    const int w0 = (nst > 2 ? 2 * GB : 0) + st.stores;
     Half fr;
     if (!early) {  // late waves: the second K half of every stage deferred past the next barrier
       hread(fr, 0, 0);
       hmma(fr);
       hread(fr, 0, 1);
-      q_wait_le(w0);
+      // (no wait: the late waves have no loads outstanding here)
       lds_barrier();
       int s = 1;
       for (; s < nst_full - 2; ++s) {
@@ -301,6 +320,12 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
   tmark(1);
 
   // ---- between the tiles: scale loads (int paths), the next tile's ring fill, then C ----
+  // LDS after the last barrier: every slot free. Order per wave: scale loads; (early waves) the
+  // next tile's A0 / B0 / B1 (head fill) into A slot 0 / B slots 0-1; C of this tile staged through
+  // A slot 1 + B slot 2 (64 KiB: every wave half its sub-tile per pass, reading back only its own
+  // region, so no barrier inside a pass) into registers; a barrier (every wave's staging reads
+  // done); (early waves) the tail fill A1 / B2 into those slots; then every wave's WTM / 8 C stores.
+  // The stores are the youngest operations: the next tile's first waits leave them in flight.
   int ci = __builtin_amdgcn_readfirstlane(cur_idx), ni = __builtin_amdgcn_readfirstlane(nx_idx);
   asm volatile("" : "+s"(ci), "+s"(ni));  // opaque: the resolves below reload (scalar loads)
   p_resolve(args, ci, t);
@@ -325,51 +350,62 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
   const bool narrow = (int64_t)Cfg::WTM * ldc < (int64_t)1 << 29;  // C byte offsets < 2^30
   const bool split = t.sk.nsplit > 1;
   QState nxt{false, 0, 0};
-  int nfill = 0;  // fill pieces this wave issued (younger than the scale loads)
-  if (ni >= 0 && narrow && !split && nst > 0) {
-    PTile nx;
-    if (p_resolve(args, ni, nx)) {
-      const int q = nx.mt.qtype;
-      if ((q == QT_F16 || q == QT_I8 || q == QT_I4 || q == QT_BF16) && nx.sk.nsplit <= 1 && nx.sk.nst > 0) {
-        const int2 f = q_fill(nx, lds, wave, lane);
-        nxt.pref = true;
-        nxt.after = f.y;
-        nfill = f.x;
-      }
+  int nfill = 0;  // head-fill pieces this wave issued (younger than the scale loads)
+  PTile nx;
+  if (ni >= 0 && narrow && !split && nst > 0 && p_resolve(args, ni, nx)) {
+    const int q = nx.mt.qtype;
+    if ((q == QT_F16 || q == QT_I8 || q == QT_I4 || q == QT_BF16) && nx.sk.nsplit <= 1 && nx.sk.nst > 0) {
+      const int2 f = q_fill_head(nx, lds, wave, lane);
+      nxt.pref = true;
+      nxt.after = f.y;
+      nfill = f.x;
     }
   }
   if constexpr (qt_scaled(QT)) q_wait_le(nfill);
   if (split && !splitk_reduce<Cfg::NT>(acc, t.sk, lds, etid)) return QState{false, 0, 0};
 
-  // ---- epilogue straight from the accumulators (gg_tile_v2's V2_DIRECT layout) ----
+  // staging: wave w's 8-KiB region, 64 rows x 128 B with the (row & 7) chunk swizzle
+  constexpr int RP = Cfg::WTM / 2;  // rows per pass (two passes fill the 64-KiB staging area)
+  static_assert(RP * 128 * 8 <= 2 * Q_ASLOT, "staging: two passes of the 64-KiB area");
+  uint8_t* const reg = (wave < HALFW ? lds + Q_ASLOT : lds + Q_BBASE + 2 * Q_BSLOT) + (wave % HALFW) * (RP * 128);
+  uint4 cv[Cfg::WTM / 8];  // this wave's sub-tile in store order: rows [8 it, 8 it + 8), 16 B per lane
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = pass * (FM / 2); i < (pass + 1) * (FM / 2); ++i) {
+      const int ml = i * 16 + e_r16 - pass * RP;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        uint2 pk;
+        if constexpr (QT == QT_F16 || QT == QT_BF16) pk = pack4_f16(acc[i][j]);
+        else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai[i], sbw[j]);
+        const int q = 2 * j + (e_g >> 1);
+        *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
+      }
+    }
+    // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
+#pragma unroll
+    for (int it = 0; it < RP / 8; ++it) {
+      const int rl = it * 8 + (e_lane >> 3), q = e_lane & 7;
+      cv[pass * (RP / 8) + it] = *reinterpret_cast<const uint4*>(reg + rl * 128 + ((q ^ (rl & 7)) << 4));
+    }
+  }
+  lds_barrier();  // every wave's staging reads are done: A slot 1 / B slot 2 are free
+  if (nxt.pref) nxt.after += q_fill_tail(nx, lds, wave, lane);
   _Float16* const cbase = t.C + (int64_t)mrow0 * ldc + ncol0;  // wave-uniform
   const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, 0x7fffffff, 0x00020000);
-  const int ccol = (e_g & 1) * 16 + (e_g >> 1) * 8;
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int ml = i * 16 + e_r16;
-#pragma unroll
-    for (int p = 0; p < FN / 2; ++p) {
-      uint2 x, y;
-      if constexpr (QT == QT_F16 || QT == QT_BF16) {
-        x = pack4_f16(acc[i][2 * p]);
-        y = pack4_f16(acc[i][2 * p + 1]);
-      } else {
-        x = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][2 * p], sai[i], sbw[2 * p]);
-        y = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][2 * p + 1], sai[i], sbw[2 * p + 1]);
-      }
-      swap16(x.x, y.x);
-      swap16(x.y, y.y);
-      const int m = mrow0 + ml, n = ncol0 + p * 32 + ccol;
-      const bool in = m < Me && n < Ne;
-      if (narrow) {
-        typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
-        const v4u_ d = {x.x, x.y, y.x, y.y};
-        __builtin_amdgcn_raw_buffer_store_b128(d, rsC, in ? (int)(((int64_t)ml * ldc + p * 32 + ccol) * 2) : (int)0x80000000,
-                                               0, 16 /* sc1 */);
-      } else if (in) {
-        *reinterpret_cast<uint4*>(cbase + (int64_t)ml * ldc + p * 32 + ccol) = uint4{x.x, x.y, y.x, y.y};
-      }
+  for (int it = 0; it < Cfg::WTM / 8; ++it) {
+    const int row = it * 8 + (e_lane >> 3), q = e_lane & 7;
+    const int m = mrow0 + row, n = ncol0 + q * 8;
+    const bool in = m < Me && n < Ne;  // N % 8 == 0: an 8-column group is all in or all out
+    if (narrow) {
+      typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+      const v4u_ d = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
+      __builtin_amdgcn_raw_buffer_store_b128(d, rsC, in ? (int)(((int64_t)row * ldc + q * 8) * 2) : (int)0x80000000, 0,
+                                             SAUX);
+    } else if (in) {
+      *reinterpret_cast<uint4*>(cbase + (int64_t)row * ldc + q * 8) = cv[it];
     }
   }
   if constexpr (TRACE != 0) {
@@ -380,14 +416,14 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
                                     ((uint64_t)(nst & 0xFFFF) << 48) | (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     }
   }
-  nxt.stores = nxt.pref ? FM * FN / 2 : 0;
+  nxt.stores = nxt.pref ? Cfg::WTM / 8 : 0;
   return nxt;
 }
 
 // One 512-thread workgroup per CU walks its planned list (TileDesc table [k][gridDim.x], ended by the
 // first empty slot). Tiles of the other bodies (w4a4 g128, E4M3, weight-only) run gg_v2_kernel's
 // bodies with their own prologue and never take a prefetch.
-template <int QM, int TRACE = 0>
+template <int QM, int TRACE = 0, int SAUX = 16>
 __global__ __launch_bounds__(512, 2) void gg_v2q_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[160 * 1024];
   const int G = gridDim.x;
@@ -406,7 +442,7 @@ __global__ __launch_bounds__(512, 2) void gg_v2q_kernel(GGArgs args) {
     bool done = false;
 #define MXMOE_V2Q(Q, BMC)                                                                                        \
   if (!done && (QM & (1 << Q)) && qt == Q && cls == BMC) {                                                       \
-    st = gg_tile_v2q<V2Cfg<(BMC) == 0 ? 256 : (BMC) == 1 ? 128 : 64>, Q, TRACE>(args, idx, nx_idx, st, lds); \
+    st = gg_tile_v2q<V2Cfg<(BMC) == 0 ? 256 : (BMC) == 1 ? 128 : 64>, Q, TRACE, SAUX>(args, idx, nx_idx, st, lds); \
     done = true;                                                                                                 \
   }
     MXMOE_V2Q(QT_I8, 0)
