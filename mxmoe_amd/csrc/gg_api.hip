@@ -181,20 +181,20 @@ void launch_v2p(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   }
 }
 
-template <int QM, int TRACE, int SAUX>
+template <int QM, int TRACE, int SAUX, int FILLALL>
 void launch_v2q_q(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gg_v2q_kernel<QM, TRACE, SAUX>), dim3(grid), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((gg_v2q_kernel<QM, TRACE, SAUX, FILLALL>), dim3(grid), dim3(512), 0, s, a);
 }
-template <int TRACE = 0, int SAUX = 16>
+template <int TRACE = 0, int SAUX = 16, int FILLALL = 0>
 void launch_v2q(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {
-    case 1: launch_v2q_q<1, TRACE, SAUX>(a, grid, s); break;
-    case 2: launch_v2q_q<2, TRACE, SAUX>(a, grid, s); break;
+    case 1: launch_v2q_q<1, TRACE, SAUX, FILLALL>(a, grid, s); break;
+    case 2: launch_v2q_q<2, TRACE, SAUX, FILLALL>(a, grid, s); break;
 #ifndef MXMOE_LAB_FAST
-    case 4: launch_v2q_q<4, TRACE, SAUX>(a, grid, s); break;
-    case 6: launch_v2q_q<6, TRACE, SAUX>(a, grid, s); break;
-    case 256: launch_v2q_q<256, TRACE, SAUX>(a, grid, s); break;
-    default: launch_v2q_q<511, TRACE, SAUX>(a, grid, s); break;  // every tile body
+    case 4: launch_v2q_q<4, TRACE, SAUX, FILLALL>(a, grid, s); break;
+    case 6: launch_v2q_q<6, TRACE, SAUX, FILLALL>(a, grid, s); break;
+    case 256: launch_v2q_q<256, TRACE, SAUX, FILLALL>(a, grid, s); break;
+    default: launch_v2q_q<511, TRACE, SAUX, FILLALL>(a, grid, s); break;  // every tile body
 #else
     default:
       fprintf(stderr, "libmxmoe_gg_lab (fast): v2q quant-type mix %#x not compiled\n", qmask);
@@ -317,10 +317,10 @@ Variant make_v2p(const char* name) {
 
 // v2q: the persistent v2x with the register epilogue and the next tile's ring fill before it
 // (gg_v2q.h); planned like v2p (per-workgroup tile lists)
-template <int TRACE = 0, int SAUX = 16>
+template <int TRACE = 0, int SAUX = 16, int FILLALL = 0>
 Variant make_v2q(const char* name, int persist_len = 0) {
   Variant v = make_v2p<0>(name);
-  v.launch = &launch_v2q<TRACE, SAUX>;
+  v.launch = &launch_v2q<TRACE, SAUX, FILLALL>;
   v.persist_len = persist_len;
   return v;
 }
@@ -356,15 +356,13 @@ const std::vector<Variant>& variants() {
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
       // experiments under test only, fp16 / w8a8 bodies only
       make_v2<kV2x>("x_v2x"),
-      make_v2<kV2x | V2_DIRECT>("x_v2x_direct"),
+      make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),
-      make_v2<kV2x | V2_DIRECT | V2_TRACE>("abl_v2x_direct_trace"),
       make_v2q("x_v2q"),
-      make_v2q<1>("abl_v2q_trace"),
-      make_v2q("x_v2q_l2", 2),
       make_v2q<0, 0>("x_v2q_plain"),
-      make_v2q<0, 0>("x_v2q_plain_l2", 2),
-      make_v2q<1, 0>("abl_v2q_plain_trace"),
+      make_v2q<0, 0, 1>("x_v2q_plain_fillall"),
+      make_v2q<0, 16, 1>("x_v2q_fillall"),
+      make_v2q<1, 0, 1>("abl_v2q_plain_fillall_trace"),
 #else
       make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
       make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),

@@ -491,16 +491,15 @@ __device__ __forceinline__ void wait_vmcnt() {
 // lane — `narrow` (wave-uniform) says every offset of the wave fits, else a plain 64-bit store.
 // Measured (profiles/r02/region/sc1_*): counter bytes -8 % on the w8a8 step, -1.4 % fp16, time
 // unchanged. -DMXMOE_STORE_PLAIN builds the plain stores for A/B.
+template <int AUX = 16>
 __device__ __forceinline__ void store_c16(_Float16* base, int64_t off, bool narrow, const uint4& v) {
-#ifndef MXMOE_STORE_PLAIN
   if (narrow) {
     typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
     const v4u_ d = {v.x, v.y, v.z, v.w};
     __builtin_amdgcn_raw_buffer_store_b128(d, __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000),
-                                           (int)(off * 2), 0, 16 /* sc1 */);
+                                           (int)(off * 2), 0, AUX /* 16: sc1 */);
     return;
   }
-#endif
   *reinterpret_cast<uint4*>(base + off) = v;
 }
 
@@ -613,10 +612,12 @@ enum : int {
   // current MFMA group (one read after the 4 MFMAs of each fragment row, which frees that row's
   // registers), leaving only the B reads between the last MFMA and the barrier
   V2_LATEIL = 1 << 29,
-  // epilogue option: C stored straight from the accumulator registers (no LDS staging): pairs of
-  // 16 x 16 blocks exchanged between lane rows by v_permlane16_swap so every lane holds 8
-  // consecutive columns of one row, one 16-B store per lane per block pair (16 rows x 64 B)
-  V2_DIRECT = 1 << 30
+  // epilogue option: plain C stores instead of sc1 (tools/store_probe.hip: a 128-KiB tile drains in
+  // 1366 vs 2434 cycles with 32 CUs storing). MEASURED NEGATIVE (round 4): C straight from the
+  // accumulator registers (pairs of 16 x 16 blocks exchanged by v_permlane16_swap, 16 rows x 64 B per
+  // store instruction): 13-15 % slower than the LDS-staged 8 rows x 128 B (probe: 5219 vs 2434 cycles
+  // per tile), profiles/r04/lab_a/
+  V2_PLAINST = 1 << 30
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -1376,50 +1377,10 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     if constexpr ((ABL & ABL_NO_EPI) != 0) {
       asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
     } else {
-      if (m < M && n < N) store_c16(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
+      if (m < M && n < N) store_c16<(ABL & V2_PLAINST) ? 0 : 16>(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
     }
   };
-  if constexpr ((ABL & V2_DIRECT) != 0) {
-    static_assert(FN % 2 == 0, "direct epilogue stores pairs of 16 x 16 blocks");
-    // after the swap lane (r16, g) holds columns [ccol, ccol + 8) of block pair p, row r16:
-    // g = 0 / 2 -> the first block's columns 0-7 / 8-15, g = 1 / 3 -> the second block's
-    const int ccol = (e_g & 1) * 16 + (e_g >> 1) * 8;
-    const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int ml = i * 16 + e_r16;
-      _Float16 sai = 0;
-      if constexpr (qt_scaled(QT)) sai = sl[wm * Cfg::WTM + ml];
-#pragma unroll
-      for (int p = 0; p < FN / 2; ++p) {
-        uint2 x, y;
-        if constexpr (QT == QT_F16 || QT == QT_BF16) {
-          x = pack4_f16(acc[i][2 * p]);
-          y = pack4_f16(acc[i][2 * p + 1]);
-        } else if constexpr (QT == QT_F8) {
-          x = scale_pack4f(acc[i][2 * p], sai, sbw[2 * p]);
-          y = scale_pack4f(acc[i][2 * p + 1], sai, sbw[2 * p + 1]);
-        } else {
-          x = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][2 * p], sai, sbw[2 * p]);
-          y = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][2 * p + 1], sai, sbw[2 * p + 1]);
-        }
-        swap16(x.x, y.x);
-        swap16(x.y, y.y);
-        const int m = mrow0 + ml, n = ncol0 + p * 32 + ccol;
-        const bool in = m < M && n < N;  // N % 8 == 0: an 8-column group is all in or all out
-        if constexpr ((ABL & ABL_NO_EPI) != 0) {
-          asm volatile("" ::"v"(x.x), "v"(x.y), "v"(y.x), "v"(y.y));
-        } else if (narrow) {
-          typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
-          const v4u_ d = {x.x, x.y, y.x, y.y};
-          __builtin_amdgcn_raw_buffer_store_b128(
-              d, rsC, in ? (int)(((int64_t)ml * mt.ldc + p * 32 + ccol) * 2) : (int)0x80000000, 0, 16 /* sc1 */);
-        } else if (in) {
-          *reinterpret_cast<uint4*>(cbase + (int64_t)ml * mt.ldc + p * 32 + ccol) = uint4{x.x, x.y, y.x, y.y};
-        }
-      }
-    }
-  } else if constexpr ((ABL & V2_EPIPE) != 0) {
+  if constexpr ((ABL & V2_EPIPE) != 0) {
     // stores of fragment row i - 1 issued behind the LDS writes of row i: the first 2 KiB of the
     // wave's 16 KiB leave after one eighth of the pack VALU, the rest drain under the remaining rows
 #pragma unroll

@@ -104,25 +104,25 @@ __device__ __forceinline__ QFillSrc q_fill_src(const PTile& t) {
   f.kb0 = t.sk.ks0 * 128;
   return f;
 }
-__device__ __forceinline__ int2 q_fill_head(const PTile& t, uint8_t* lds, int wave, int lane) {
+__device__ __forceinline__ int2 q_fill_head(const PTile& t, uint8_t* lds, int wave, int lane, bool edma) {
   const GGMeta& m = t.mt;
   const QFillSrc f = q_fill_src(t);
   if (f.nst <= 0) return int2{0, 0};
-  int first = q_dma(f.a, f.GA, m.lda_b, f.kb0, m.kbytes, true, wave, lane, lds);
-  first += q_dma(f.b, 4, m.ldb_b, f.kb0, m.kbytes, true, wave, lane, lds + Q_BBASE);
-  const int after = f.nst > 1 ? q_dma(f.b, 4, m.ldb_b, f.kb0 + 128, m.kbytes, true, wave, lane, lds + Q_BBASE + Q_BSLOT) : 0;
+  int first = q_dma(f.a, f.GA, m.lda_b, f.kb0, m.kbytes, edma, wave, lane, lds);
+  first += q_dma(f.b, 4, m.ldb_b, f.kb0, m.kbytes, edma, wave, lane, lds + Q_BBASE);
+  const int after = f.nst > 1 ? q_dma(f.b, 4, m.ldb_b, f.kb0 + 128, m.kbytes, edma, wave, lane, lds + Q_BBASE + Q_BSLOT) : 0;
   return int2{first + after, after};
 }
-__device__ __forceinline__ int q_fill_tail(const PTile& t, uint8_t* lds, int wave, int lane) {
+__device__ __forceinline__ int q_fill_tail(const PTile& t, uint8_t* lds, int wave, int lane, bool edma) {
   const GGMeta& m = t.mt;
   const QFillSrc f = q_fill_src(t);
   int n = 0;
-  if (f.nst > 1) n += q_dma(f.a, f.GA, m.lda_b, f.kb0 + 128, m.kbytes, true, wave, lane, lds + Q_ASLOT);
-  if (f.nst > 2) n += q_dma(f.b, 4, m.ldb_b, f.kb0 + 256, m.kbytes, true, wave, lane, lds + Q_BBASE + 2 * Q_BSLOT);
+  if (f.nst > 1) n += q_dma(f.a, f.GA, m.lda_b, f.kb0 + 128, m.kbytes, edma, wave, lane, lds + Q_ASLOT);
+  if (f.nst > 2) n += q_dma(f.b, 4, m.ldb_b, f.kb0 + 256, m.kbytes, edma, wave, lane, lds + Q_BBASE + 2 * Q_BSLOT);
   return n;
 }
 
-template <class Cfg, int QT, int TRACE = 0, int SAUX = 16>
+template <class Cfg, int QT, int TRACE = 0, int SAUX = 16, int FILLALL = 0>
 __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, int nx_idx, QState st, uint8_t* lds) {
   constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
   typedef typename AccT<QT>::type acc_t;
@@ -220,7 +220,7 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
   // ---- prologue: the ring fill (issued by the previous tile when st.pref), A0 / B0 landed ----
   if (nst > 0) {
     if (!st.pref) {
-      st.after = q_fill_head(t, lds, wave, lane).y + q_fill_tail(t, lds, wave, lane);
+      st.after = q_fill_head(t, lds, wave, lane, !FILLALL).y + q_fill_tail(t, lds, wave, lane, !FILLALL);
       st.stores = 0;
     }
     q_wait_le(st.after + st.stores);
@@ -228,13 +228,15 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
     // iteration 0: A1 / B1 landed; B2 and the previous tile's stores may stay in flight
     // (early waves: the fill's B2 and this wave's stores of the previous tile may stay in flight;
     //  the late waves have no loads outstanding: the fill is the early waves')
-    const int w0 = (nst > 2 ? 2 * GB : 0) + st.stores;
+    // (FILLALL: every wave issued its own fill pieces; the late waves then require B2 as well here,
+    //  since their EDMA mainloop has no later wait)
+    const int w0 = (nst > 2 ? (FILLALL ? (early ? GB : 0) : 2 * GB) : 0) + st.stores;
     Half fr;
     if (!early) {  // late waves: the second K half of every stage deferred past the next barrier
       hread(fr, 0, 0);
       hmma(fr);
       hread(fr, 0, 1);
-      // (no wait: the late waves have no loads outstanding here)
+      if constexpr (FILLALL != 0) q_wait_le(w0);  // (else: no loads of the late waves outstanding here)
       lds_barrier();
       int s = 1;
       for (; s < nst_full - 2; ++s) {
@@ -355,7 +357,7 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
   if (ni >= 0 && narrow && !split && nst > 0 && p_resolve(args, ni, nx)) {
     const int q = nx.mt.qtype;
     if ((q == QT_F16 || q == QT_I8 || q == QT_I4 || q == QT_BF16) && nx.sk.nsplit <= 1 && nx.sk.nst > 0) {
-      const int2 f = q_fill_head(nx, lds, wave, lane);
+      const int2 f = q_fill_head(nx, lds, wave, lane, !FILLALL);
       nxt.pref = true;
       nxt.after = f.y;
       nfill = f.x;
@@ -391,7 +393,7 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
     }
   }
   lds_barrier();  // every wave's staging reads are done: A slot 1 / B slot 2 are free
-  if (nxt.pref) nxt.after += q_fill_tail(nx, lds, wave, lane);
+  if (nxt.pref) nxt.after += q_fill_tail(nx, lds, wave, lane, !FILLALL);
   _Float16* const cbase = t.C + (int64_t)mrow0 * ldc + ncol0;  // wave-uniform
   const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
@@ -423,7 +425,7 @@ __device__ __forceinline__ QState gg_tile_v2q(const GGArgs& args, int cur_idx, i
 // One 512-thread workgroup per CU walks its planned list (TileDesc table [k][gridDim.x], ended by the
 // first empty slot). Tiles of the other bodies (w4a4 g128, E4M3, weight-only) run gg_v2_kernel's
 // bodies with their own prologue and never take a prefetch.
-template <int QM, int TRACE = 0, int SAUX = 16>
+template <int QM, int TRACE = 0, int SAUX = 16, int FILLALL = 0>
 __global__ __launch_bounds__(512, 2) void gg_v2q_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[160 * 1024];
   const int G = gridDim.x;
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(512, 2) void gg_v2q_kernel(GGArgs args) {
     bool done = false;
 #define MXMOE_V2Q(Q, BMC)                                                                                        \
   if (!done && (QM & (1 << Q)) && qt == Q && cls == BMC) {                                                       \
-    st = gg_tile_v2q<V2Cfg<(BMC) == 0 ? 256 : (BMC) == 1 ? 128 : 64>, Q, TRACE, SAUX>(args, idx, nx_idx, st, lds); \
+    st = gg_tile_v2q<V2Cfg<(BMC) == 0 ? 256 : (BMC) == 1 ? 128 : 64>, Q, TRACE, SAUX, FILLALL>(args, idx, nx_idx, st, lds); \
     done = true;                                                                                                 \
   }
     MXMOE_V2Q(QT_I8, 0)
