@@ -214,6 +214,15 @@ template <int NWG>
 int wo2_launch_lds(int qmask) { return wo2_full_nwg(qmask & 511) ? wo2_lds_bytes<NWG>() : wo2_lds_bytes<2>(); }
 template <int ABL, int NWG>
 void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+#ifdef MXMOE_LAB_FAST
+  switch (qmask & 511) {  // fast lab build: the w4a16 and w4a16 + w8a8 sets only
+    case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;
+    case 10: launch_wo2_q<ABL, 10, NWG>(a, grid, s); break;
+    default:
+      fprintf(stderr, "libmxmoe_gg_lab (fast): wo2 quant-type mix %#x not compiled\n", qmask);
+      abort();
+  }
+#else
   switch (qmask & 511) {
     case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;    // w4a16 only
     case 64: launch_wo2_q<ABL, 64, NWG>(a, grid, s); break;  // w2a16 only
@@ -227,6 +236,7 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
     case 16: launch_wo2_q<ABL, 16, 2>(a, grid, s); break;  // w8a16 only
     default: launch_wo2_q<ABL, 95, 2>(a, grid, s); break;  // any mix of fp16, w8a8, w4a4 and weight-only
   }
+#endif
 }
 
 template <class C16, class C8, class C4>
@@ -325,6 +335,9 @@ Variant make_v2q(const char* name, int persist_len = 0) {
   return v;
 }
 
+// the small-batch weight-only tile's loop options (gg_tile_wo)
+constexpr int kWo3 = WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT;
+
 // the round-3 AUTO default's mainloop flags (variant v2x_256x256_w8_b3_buf_spread_edma, without the
 // weight-only options)
 constexpr int kV2x = V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | (4 << V2_SPREAD_SHIFT);
@@ -350,8 +363,10 @@ const std::vector<Variant>& variants() {
       // +1-4 % on the small-batch w4a16 calls, profiles/r03/wo/)
       make_v2<kV2x | WO_PIPE | WO_STAG>("v2x_256x256_w8_b3_buf_spread_edma"),
       // round 3 (AUTO for small-batch weight-only calls): the 64-row weight-only tile at three
-      // workgroups per CU (gg_wo2_kernel<.., 3>; weight-only problems only) — profiles/r03/wo2/
-      make_wo2<0, 3>("wo3_64x256_w8_3wg"),
+      // workgroups per CU (gg_wo2_kernel<.., 3>; weight-only problems only) — profiles/r03/wo2/;
+      // round 4: scale groups by LDS-DMA, register constants for the code -> fp16 step, no MFMAs
+      // for row blocks past M, steady / tail loops (-9 to -14 % at bs 512, profiles/r04/wo/)
+      make_wo2<kWo3, 3>("wo3_64x256_w8_3wg"),
 #elif defined(MXMOE_LAB_FAST)
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
       // experiments under test only, fp16 / w8a8 bodies only
@@ -363,6 +378,12 @@ const std::vector<Variant>& variants() {
       make_v2q<0, 0, 1>("x_v2q_plain_fillall"),
       make_v2q<0, 16, 1>("x_v2q_fillall"),
       make_v2q<1, 0, 1>("abl_v2q_plain_fillall_trace"),
+      // the small-batch weight-only tile: where its time goes (ablations: WRONG RESULTS by design)
+      make_wo2<0, 3>("x_wo3_r3"),  // the round-3 loop
+      make_wo2<kWo3, 3>("x_wo3"),
+      make_wo2<kWo3 | V2_TRACE, 3>("abl_wo3_trace"),
+      make_wo2<kWo3 | ABL_WO_NODMA, 3>("abl_wo3_nodma"),
+      make_wo2<kWo3 | ABL_WO_NOCOMPUTE, 3>("abl_wo3_nocompute"),
 #else
       make_v0<T128x128, T128x128, T128x128>("v0_128x128_w4"),
       make_v0<T256x128, T256x128, T256x128>("v0_256x128_w4"),
@@ -922,7 +943,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // only layer-11 calls it cuts (the partial-sum round trip costs more than the ragged finish
   // it removes). Lab library only, opt-in: MXMOE_GG_TAIL_SPLIT=1.
   const char* ts_env = planner_knob("MXMOE_GG_TAIL_SPLIT");
-  if (v.kind == Kind::V2 && !v.persistent && ts_env && ts_env[0] == '1') {
+  if (v.kind == Kind::V2 && !v.persistent && ts_env && (ts_env[0] == '1' || ts_env[0] == '2')) {
     auto simulate = [&](const std::vector<double>& t, std::vector<double>* starts) {
       std::vector<double> slot(chunk, 0.0);  // min-heap of slot free times
       double finish = 0;
@@ -946,7 +967,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       while (j0 > 0 && st[j0 - 1] >= base.second) --j0;  // starts are non-decreasing in queue order
       auto splittable = [&](const TileDesc& td) {
         const int qt = plan->meta[td.prob].qtype;
-        return ((td.cls >> 16) & 0xFF) <= 1 && !is_weightonly(qt) && qt != QT_I4G && td.ks1 - td.ks0 >= 6;
+        // ('2': weight-only tiles too — the small-batch wo3 calls run ~1.3 rounds of equal tiles)
+        return ((td.cls >> 16) & 0xFF) <= 1 && (!is_weightonly(qt) || ts_env[0] == '2') && qt != QT_I4G &&
+               td.ks1 - td.ks0 >= 6;
       };
       int best_s = 1;
       double best_finish = base.first;

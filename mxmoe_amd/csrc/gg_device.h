@@ -617,7 +617,19 @@ enum : int {
   // accumulator registers (pairs of 16 x 16 blocks exchanged by v_permlane16_swap, 16 rows x 64 B per
   // store instruction): 13-15 % slower than the LDS-staged 8 rows x 128 B (probe: 5219 vs 2434 cycles
   // per tile), profiles/r04/lab_a/
-  V2_PLAINST = 1 << 30
+  V2_PLAINST = 1 << 30,
+  // weight-only option (non-pipelined loop, wo3): the next group's scale words are kept raw and
+  // packed after the stage's MFMAs, so the compiler's wait before the packing leaves the ring's DMA
+  // in flight (packed right after the load it became vmcnt(0): the whole ring drained at every group
+  // boundary, every second stage at g128); the group index is a counter, not a division per boundary
+  WO_SCLATE = 32,
+  // weight-only option: the code -> fp16 constants in registers (WoK): one v_and_or_b32 per fp16
+  // pair (4 / 2-bit codes), one v_perm_b32 (8-bit) — VALU-bound small-batch tiles
+  WO_ANDOR = 128,
+  // weight-only option (non-pipelined loop): skip the MFMAs and A reads of 16-row blocks wholly past M
+  WO_MSKIP = 256,
+  // with WO_SCLATE: the steady state (stage s + DIST exists) and the tail as two loops
+  WO_SPLIT = 8192
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -1972,6 +1984,7 @@ struct WoCfg {
   static constexpr int nbuf() {
     return LDSB_ / stage_bytes<BITS>() > 8 ? 8 : LDSB_ / stage_bytes<BITS>();
   }
+  static constexpr int LDSB = LDSB_;
   static_assert(2 * STAGE_BYTES <= LDSB_, "two stages must fit the LDS image");
   static_assert(WM * WN * WTM * WTN * 2 <= LDSB_, "the epilogue's staged tile must fit the LDS image");
 };
@@ -1981,23 +1994,38 @@ __device__ __forceinline__ uint32_t wo_perm(uint32_t hi, uint32_t lo, uint32_t s
 }
 
 // 8 codes (K ascending) -> 8 fp16 dequantised values
+// Register constants of the code -> fp16 step: with WO_ANDOR the tile makes them opaque (asm) so
+// they stay in registers — gfx950's VOP3 takes no literal, so with literal constants the compiler
+// splits v_and_or_b32 into v_and_b32 + v_or_b32 and keeps v_perm_b32 + v_or_b32 for 8-bit codes
+struct WoK {
+  uint32_t magic = 0x64006400u;  // fp16 1024 in both halves
+  uint32_t mask4 = 0x000F000Fu, mask2 = 0x00030003u;
+  uint32_t hi8 = 0x64646464u;   // 8-bit codes: v_perm_b32 takes the 0x64 bytes from here
+  bool perm8 = false;           // 8-bit: one v_perm_b32 per pair (sel bytes 4 -> hi8)
+};
+
 template <int BITS>
-__device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uint32_t s2, uint32_t z2) {
+__device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uint32_t s2, uint32_t z2,
+                                          const WoK& k = WoK()) {
   uint32_t d[4];
   if constexpr (BITS == 4) {
     // repacked order: codes 2q, 2q+1 at bits 4q and 16 + 4q -> one v_and_or_b32 per fp16 pair
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (4 * q)) & 0x000F000Fu) | 0x64006400u;
+    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (4 * q)) & k.mask4) | k.magic;
   } else if constexpr (BITS == 2) {
     // w[0] = the unit's 32-bit word pre-shifted by 8 * kc: codes 2q, 2q+1 at bits 2q and 16 + 2q
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (2 * q)) & 0x00030003u) | 0x64006400u;
+    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (2 * q)) & k.mask2) | k.magic;
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // bytes 2q, 2q+1 of the 8 codes
       const uint32_t src = w[q >> 1];
-      const uint32_t sel = (q & 1) ? 0x0c030c02u : 0x0c010c00u;
-      d[q] = wo_perm(0, src, sel) | 0x64006400u;
+      if (k.perm8) {
+        d[q] = wo_perm(k.hi8, src, (q & 1) ? 0x04030402u : 0x04010400u);
+      } else {
+        const uint32_t sel = (q & 1) ? 0x0c030c02u : 0x0c010c00u;
+        d[q] = wo_perm(0, src, sel) | 0x64006400u;
+      }
     }
   }
   typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -2080,6 +2108,12 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   // fp16 -(1024 + off) = 0xE400 | off: sym off = 7 (4-bit) / 127 (8-bit), asym 0
   const uint32_t moff2 = sym ? (BITS == 4 ? 0xE407E407u : BITS == 2 ? 0xE401E401u : 0xE47FE47Fu) : 0xE400E400u;
   uint32_t s2[FN], z2[FN], s2n[FN], z2n[FN];  // current group, next group (prefetched)
+  WoK wok;
+  if constexpr ((WABL & WO_ANDOR) != 0) {
+    wok.perm8 = true;
+    if constexpr (BITS == 8) asm volatile("" : "+v"(wok.hi8));
+    else asm volatile("" : "+v"(wok.magic), "+s"(wok.mask4), "+s"(wok.mask2));
+  }
   auto load_scales = [&](int grp, uint32_t (&so)[FN], uint32_t (&zo)[FN]) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -2103,6 +2137,8 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0, 0, 0, 0};
 
   const int swz = (r16 >> 1) & 7;
+  // WO_MSKIP: the wave's 16-row blocks holding a row < M (small batches: ~35-row experts on 64-row tiles)
+  const int nfm = __builtin_amdgcn_readfirstlane(min(FM, max(1, (M - m0 - wm * Cfg::WTM + 15) / 16)));
   const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * RB;
   // rows of a B fragment are base + r16 with base % 16 == 0, so the swizzle depends on r16 only
@@ -2131,18 +2167,21 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       for (int j = 0; j < FN; ++j) {
         if constexpr (BITS == 2) {
           const uint32_t w = raw[j][0] >> (8 * kc);
-          b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j]);
+          b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j], wok);
         } else if constexpr (BITS == 4) {
-          b[j] = wo_dequant<4>(&raw[j][kc], moff2, s2[j], z2[j]);
+          b[j] = wo_dequant<4>(&raw[j][kc], moff2, s2[j], z2[j], wok);
         } else {
           const uint2 v = *reinterpret_cast<const uint2*>(Bs + j * 16 * RB + ((g ^ bsw) << 4) + kc * 8);
           raw[j][0] = v.x;
           raw[j][1] = v.y;
-          b[j] = wo_dequant<8>(raw[j], moff2, s2[j], z2[j]);
+          b[j] = wo_dequant<8>(raw[j], moff2, s2[j], z2[j], wok);
         }
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
+        if constexpr ((WABL & WO_MSKIP) != 0) {
+          if (i > 0 && i >= nfm) break;  // row block wholly past M (uniform)
+        }
         const v8h a = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, acc[i][j], 0, 0, 0);
@@ -2201,11 +2240,11 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     for (int j = 0; j < FN; ++j) {
       if constexpr (BITS == 2) {
         const uint32_t w = f.rb[j][0][0] >> (8 * kc);
-        b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j]);
+        b[j] = wo_dequant<2>(&w, moff2, s2[j], z2[j], wok);
       } else if constexpr (BITS == 4) {
-        b[j] = wo_dequant<4>(&f.rb[j][0][kc], moff2, s2[j], z2[j]);
+        b[j] = wo_dequant<4>(&f.rb[j][0][kc], moff2, s2[j], z2[j], wok);
       } else {
-        b[j] = wo_dequant<8>(f.rb[j][kc], moff2, s2[j], z2[j]);
+        b[j] = wo_dequant<8>(f.rb[j][kc], moff2, s2[j], z2[j], wok);
       }
     }
   };
@@ -2302,6 +2341,87 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     wait_vmcnt<0>();
     lds_barrier();  // ring -> epilogue staging
    }
+  } else if (nst > 0 && (WABL & WO_SCLATE) != 0) {
+    // A stage that opens a scale group brings the group's scale words along: one LDS-DMA piece per
+    // lane (lanes 0-31: the wave's 32 columns, 2 / 4 B at lane * 4 — the DMA's LDS stride below
+    // 16-B pieces) into a 1-KiB slot beside the stage's ring buffer, issued just before the stage's
+    // own DMA, so the counted wait that publishes the stage covers it too: the ring never drains
+    // for scales (round 3: a register load right before use, vmcnt(0) at every group boundary)
+    static_assert((WABL & WO_SCLATE) == 0 || NBUF * SB_ + NBUF * 1024 <= Cfg::LDSB, "the scale slots sit past the ring");
+    uint8_t* const sc_base = lds + NBUF * SB_ + wave * 128;
+    load_scales(ks0 / gstages, s2, z2);
+    const int nl = min(ncol0 + (lane & 31), N - 1);
+    int ipos = ks0 % gstages, igrp = ks0 / gstages;  // issue stream: stage t's place in its group
+    int cpos = ipos;                                   // compute stream
+    auto issue_sc = [&](int t, int buf) {
+      if (t > 0 && ipos == 0 && lane < 32) {
+        if (sym) __builtin_amdgcn_global_load_lds((gbl_void_t*)(SB + (int64_t)igrp * N + nl), (lds_void_t*)(sc_base + buf * 1024), 2, 0, 0);
+        else __builtin_amdgcn_global_load_lds((gbl_void_t*)(SB + ((int64_t)igrp * N + nl) * 2), (lds_void_t*)(sc_base + buf * 1024), 4, 0, 0);
+      }
+      if (++ipos == gstages) {
+        ipos = 0;
+        ++igrp;
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < DIST; ++p)
+      if (p < nst) {
+        issue_sc(p, p);
+        issue(p, p);
+      }
+    int bc = 0, bi = DIST % NBUF;  // s % NBUF, (s + DIST) % NBUF
+    // STEADY: stage s + DIST exists (one constant wait, an unconditional issue); the tail waits by
+    // the count of stages still in flight (WO_SPLIT: two loops; else one loop with both tests)
+    auto step = [&](int s, auto steady_c) {
+      constexpr bool STEADY = decltype(steady_c)::value;
+      if constexpr ((WABL & WO_SPLIT) != 0) {
+        if constexpr (STEADY) wait_vmcnt<(DIST - 1) * DPS>();
+        else wait_stage(nst - 1 - s);
+      } else {
+        if (s + DIST - 1 < nst) wait_vmcnt<(DIST - 1) * DPS>();
+        else wait_stage(nst - 1 - s);
+      }
+      lds_barrier();
+      if (s > 0 && cpos == 0) {  // stage s opens a group: its scales sit in the slot of its buffer
+        const uint8_t* sc = sc_base + bc * 1024;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if (sym) {
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(sc + (j * 16 + r16) * 4);
+            s2[j] = v * 0x10001u;
+            z2[j] = 0;
+          } else {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(sc + (j * 16 + r16) * 4);
+            s2[j] = (v & 0xFFFFu) * 0x10001u;
+            z2[j] = (v >> 16) * 0x10001u;
+          }
+        }
+      }
+      if (++cpos == gstages) cpos = 0;
+      if constexpr ((WABL & WO_SPLIT) != 0) {
+        if constexpr (STEADY) {
+          issue_sc(s + DIST, bi);
+          issue(s + DIST, bi);
+        }
+      } else {
+        if (s + DIST < nst) {
+          issue_sc(s + DIST, bi);
+          issue(s + DIST, bi);
+        }
+      }
+      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(bc);
+      bc = bc + 1 == NBUF ? 0 : bc + 1;
+      bi = bi + 1 == NBUF ? 0 : bi + 1;
+    };
+    if constexpr ((WABL & WO_SPLIT) != 0) {
+      int s = 0;
+      for (; s + DIST < nst; ++s) step(s, std::true_type());
+      for (; s < nst; ++s) step(s, std::false_type());
+    } else {
+      for (int s = 0; s < nst; ++s) step(s, std::true_type());
+    }
+    wait_vmcnt<0>();
+    lds_barrier();  // ring -> epilogue staging
   } else if (nst > 0) {
     load_scales(ks0 / gstages, s2, z2);
 #pragma unroll
@@ -2430,6 +2550,7 @@ template <int ABL, int QM, int NWG = 2>
 __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   constexpr int WO2_LDS_BYTES = wo2_lds_bytes<NWG>();
   __shared__ __attribute__((aligned(16))) uint8_t lds[WO2_LDS_BYTES];
+  if constexpr ((ABL & V2_TRACE) != 0) trace_mark(0);
   const TileDesc td = args.tiles[blockIdx.x];
   if (td.prob < 0) return;
   const GGMeta mt = args.meta[td.prob];
@@ -2447,7 +2568,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  constexpr int WP = ABL & (WO_PIPE | WO_STAG);
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
@@ -2464,6 +2585,16 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  if constexpr ((ABL & V2_TRACE) != 0) {  // (as gg_v2_kernel; the class field holds the problem index)
+    if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) {
+      wait_vmcnt<0>();
+      uint64_t hw = ((uint64_t)(__builtin_amdgcn_s_getreg((19 << 11) | 20) & 0xF) << 32) |
+                    ((uint64_t)(mt.qtype & 0xF) << 36) | ((uint64_t)(td.prob & 0xFF) << 40) |
+                    ((uint64_t)(sk.nst & 0xFFFF) << 48) | (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+      g_gg_trace[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+      g_gg_trace[blockIdx.x * 4 + 3] = hw;
+    }
+  }
 }
 
 // ============================================================================================

@@ -64,7 +64,12 @@ def main():
           "w4a16c": dict(qstr="w4a16_g-1_sym"), "w8a16": dict(qstr="w8a16_g-1_asym"),
           "w4a16ga": dict(qstr="w4a16_g-1_asym"), "w4a16gs": dict(qstr="w4a16_g128_sym"),
           "w4a4g128": dict(qstr="w4a4_g128_sym"), "w2a16": dict(qstr="w2a16_g128_asym"),
-          "e4m3": dict(qstr="w8a8_g-1_sym_E4M3"), "bf16": dict(qstr="bf16"), "ds2_mixed": {}}[args.cfg]
+          "e4m3": dict(qstr="w8a8_g-1_sym_E4M3"), "bf16": dict(qstr="bf16"), "ds2_mixed": {},
+          "w4a16_w8a8": {}}[args.cfg]
+    if args.cfg == "w4a16_w8a8":  # bench config w4a16_w8a8_bs512's scheme (w4a16 + 1/16 w8a8)
+        from mxmoe_amd.workload import w4a16_w8a8_qconfig
+
+        kw = dict(qconfig=w4a16_w8a8_qconfig())
     if args.dense:
         bits = {"fp16": 16, "w8a8": 8, "w4a4": 4, "e4m3": 8, "bf16": 16}[args.cfg]
         fmt = {"e4m3": "E4M3", "bf16": "bf16"}.get(args.cfg, "")

@@ -44,6 +44,9 @@ def cases():
                 (M, N, K, q) for M, N, K in [(1, 128, 256), (17, 256, 128 if g == -1 else 256), (130, 136, 384),
                                              (257, 264, 512), (513, 512, 1408), (64, 8, 1024), (34, 2816, 2048),
                                              (41, 2048, 1408), (96, 512, 640)]]
+    # the small-batch pairing (w4a16 + w8a8 in one launch: wo3's QM = 10 build)
+    yield "w4a16w8a8", [(34, 2816, 2048, QParams(16, 4, -1, False)), (41, 2048, 1408, QParams(16, 4, 128, False)),
+                        (57, 256, 512, W8A8), (3, 128, 256, QParams(16, 4, 128, True)), (130, 384, 1024, W8A8)]
 
 
 def main():

@@ -96,7 +96,11 @@ def main():
         os.environ[k] = v
     kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
           "mixed": dict(qconfig=mixed_qconfig_lp1()), "w4a16": dict(qstr="w4a16_g128_asym"),
-          "w4a16c": dict(qstr="w4a16_g-1_sym"), "w4a16ga": dict(qstr="w4a16_g-1_asym")}[args.cfg]
+          "w4a16c": dict(qstr="w4a16_g-1_sym"), "w4a16ga": dict(qstr="w4a16_g-1_asym"), "w4a16_w8a8": {}}[args.cfg]
+    if args.cfg == "w4a16_w8a8":  # bench config w4a16_w8a8_bs512's scheme
+        from mxmoe_amd.workload import w4a16_w8a8_qconfig
+
+        kw = dict(qconfig=w4a16_w8a8_qconfig())
     if args.dense:
         bits = {"fp16": 16, "w8a8": 8, "w4a4": 4}[args.cfg]
         shapes = [QShape([int(x) for x in args.dense.split(",")], bits, bits)]
