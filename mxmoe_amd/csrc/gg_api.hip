@@ -336,7 +336,7 @@ Variant make_v2q(const char* name, int persist_len = 0) {
 }
 
 // the small-batch weight-only tile's loop options (gg_tile_wo)
-constexpr int kWo3 = WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT;
+constexpr int kWo3 = WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS;
 
 // the round-3 AUTO default's mainloop flags (variant v2x_256x256_w8_b3_buf_spread_edma, without the
 // weight-only options)
@@ -364,8 +364,9 @@ const std::vector<Variant>& variants() {
       make_v2<kV2x | WO_PIPE | WO_STAG>("v2x_256x256_w8_b3_buf_spread_edma"),
       // round 3 (AUTO for small-batch weight-only calls): the 64-row weight-only tile at three
       // workgroups per CU (gg_wo2_kernel<.., 3>; weight-only problems only) — profiles/r03/wo2/;
-      // round 4: scale groups by LDS-DMA, register constants for the code -> fp16 step, no MFMAs
-      // for row blocks past M, steady / tail loops (-9 to -14 % at bs 512, profiles/r04/wo/)
+      // round 4: scale groups by LDS-DMA, register constants for the code -> fp16 step, codes
+      // converted where they sit, no MFMAs for row blocks past M, steady / tail loops (-10 to
+      // -16 % per call at bs 512, -15 to -25 % at bs 128: profiles/r04/wo/)
       make_wo2<kWo3, 3>("wo3_64x256_w8_3wg"),
 #elif defined(MXMOE_LAB_FAST)
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the

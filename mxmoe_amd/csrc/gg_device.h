@@ -629,7 +629,9 @@ enum : int {
   // weight-only option (non-pipelined loop): skip the MFMAs and A reads of 16-row blocks wholly past M
   WO_MSKIP = 256,
   // with WO_SCLATE: the steady state (stage s + DIST exists) and the tail as two loops
-  WO_SPLIT = 8192
+  WO_SPLIT = 8192,
+  // weight-only option: 4 / 2-bit codes converted where they sit (WoK::nibpos)
+  WO_NIBPOS = INT32_MIN
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -2002,6 +2004,14 @@ struct WoK {
   uint32_t mask4 = 0x000F000Fu, mask2 = 0x00030003u;
   uint32_t hi8 = 0x64646464u;   // 8-bit codes: v_perm_b32 takes the 0x64 bytes from here
   bool perm8 = false;           // 8-bit: one v_perm_b32 per pair (sel bytes 4 -> hi8)
+  // nibpos (WO_NIBPOS): a code is read where it sits — the fp16 whose exponent puts the code's
+  // lowest bit at weight 1 (bits 0 / 2 / 4 / 6: 1024 / 256 / 64 / 16 + u, exact), so a 4-bit word
+  // needs one shift (by 8) instead of three and a 2-bit word none; the subtrahend per position
+  // is -(base + off) (moffq), still exact, so fma(x, s, z) rounds as before
+  bool nibpos = false;
+  uint32_t nmask[4] = {0x000F000Fu, 0x00F000F0u, 0, 0};     // 4-bit: [0] bits 0-3, [1] bits 4-7
+  uint32_t nmagic[4] = {0x64006400u, 0x54005400u, 0, 0};    // 1024, 64 (2-bit: 1024, 256, 64, 16)
+  uint32_t moffq[4] = {0, 0, 0, 0};
 };
 
 template <int BITS>
@@ -2010,12 +2020,25 @@ __device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uin
   uint32_t d[4];
   if constexpr (BITS == 4) {
     // repacked order: codes 2q, 2q+1 at bits 4q and 16 + 4q -> one v_and_or_b32 per fp16 pair
+    if (k.nibpos) {
+      const uint32_t w8 = w[0] >> 8;
+      d[0] = (w[0] & k.nmask[0]) | k.nmagic[0];
+      d[1] = (w[0] & k.nmask[1]) | k.nmagic[1];
+      d[2] = (w8 & k.nmask[0]) | k.nmagic[0];
+      d[3] = (w8 & k.nmask[1]) | k.nmagic[1];
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (4 * q)) & k.mask4) | k.magic;
+      for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (4 * q)) & k.mask4) | k.magic;
+    }
   } else if constexpr (BITS == 2) {
     // w[0] = the unit's 32-bit word pre-shifted by 8 * kc: codes 2q, 2q+1 at bits 2q and 16 + 2q
+    if (k.nibpos) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (2 * q)) & k.mask2) | k.magic;
+      for (int q = 0; q < 4; ++q) d[q] = (w[0] & k.nmask[q]) | k.nmagic[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = ((w[0] >> (2 * q)) & k.mask2) | k.magic;
+    }
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // bytes 2q, 2q+1 of the 8 codes
@@ -2032,7 +2055,8 @@ __device__ __forceinline__ v8h wo_dequant(const uint32_t* w, uint32_t moff2, uin
   v8h out;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    h2 x = __builtin_bit_cast(h2, d[q]) + __builtin_bit_cast(h2, moff2);  // exact: u - off
+    const uint32_t mo = (BITS != 8 && k.nibpos) ? k.moffq[q] : moff2;
+    h2 x = __builtin_bit_cast(h2, d[q]) + __builtin_bit_cast(h2, mo);  // exact: u - off
     x = __builtin_elementwise_fma(x, __builtin_bit_cast(h2, s2), __builtin_bit_cast(h2, z2));
     out[2 * q] = x[0];
     out[2 * q + 1] = x[1];
@@ -2109,9 +2133,28 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const uint32_t moff2 = sym ? (BITS == 4 ? 0xE407E407u : BITS == 2 ? 0xE401E401u : 0xE47FE47Fu) : 0xE400E400u;
   uint32_t s2[FN], z2[FN], s2n[FN], z2n[FN];  // current group, next group (prefetched)
   WoK wok;
+  if constexpr ((WABL & WO_NIBPOS) != 0 && BITS != 8) {
+    wok.nibpos = true;
+    const int off = sym ? (BITS == 4 ? 7 : 1) : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int base = BITS == 4 ? ((q & 1) ? 64 : 1024) : (1024 >> (2 * q));  // 2-bit: 1024, 256, 64, 16
+      if constexpr (BITS == 2) {
+        wok.nmask[q] = 0x00030003u << (2 * q);
+        wok.nmagic[q] = q == 0 ? 0x64006400u : q == 1 ? 0x5C005C00u : q == 2 ? 0x54005400u : 0x4C004C00u;
+      }
+      const uint32_t h = __builtin_bit_cast(uint16_t, (_Float16)(-(float)(base + off)));
+      wok.moffq[q] = h | (h << 16);
+    }
+  }
   if constexpr ((WABL & WO_ANDOR) != 0) {
     wok.perm8 = true;
     if constexpr (BITS == 8) asm volatile("" : "+v"(wok.hi8));
+    else if constexpr ((WABL & WO_NIBPOS) != 0 && BITS == 4)
+      asm volatile("" : "+v"(wok.nmagic[0]), "+v"(wok.nmagic[1]), "+s"(wok.nmask[0]), "+s"(wok.nmask[1]));
+    else if constexpr ((WABL & WO_NIBPOS) != 0 && BITS == 2)
+      asm volatile("" : "+v"(wok.nmagic[0]), "+v"(wok.nmagic[1]), "+v"(wok.nmagic[2]), "+v"(wok.nmagic[3]),
+                   "+s"(wok.nmask[0]), "+s"(wok.nmask[1]), "+s"(wok.nmask[2]), "+s"(wok.nmask[3]));
     else asm volatile("" : "+v"(wok.magic), "+s"(wok.mask4), "+s"(wok.mask2));
   }
   auto load_scales = [&](int grp, uint32_t (&so)[FN], uint32_t (&zo)[FN]) {
@@ -2143,7 +2186,8 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * RB;
   // rows of a B fragment are base + r16 with base % 16 == 0, so the swizzle depends on r16 only
   const int bsw = (r16 >> RSH) & (LPR - 1);
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf, auto nf_c) {  // NF: row blocks computed (FM)
+    constexpr int NF = decltype(nf_c)::value;
     const uint8_t* As = lds + buf * SB_ + a_row;
     const uint8_t* Bs = lds + buf * SB_ + Cfg::A_BYTES + b_row;
     uint32_t raw[FN][2];  // 4-bit: the codes of both K halves (one 8-B read); 8-bit: one K half
@@ -2179,8 +2223,11 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
+        // row block wholly past M: a uniform test per block (MEASURED NEGATIVE, round 4: one loop
+        // copy per row-block count, NF = 1..4, was as fast on gate_up and 9-17 % slower on the
+        // down calls, profiles/r04/wo/wo_g)
         if constexpr ((WABL & WO_MSKIP) != 0) {
-          if (i > 0 && i >= nfm) break;  // row block wholly past M (uniform)
+          if (i > 0 && i >= nfm) break;
         }
         const v8h a = *reinterpret_cast<const v8h*>(As + i * 2048 + off);
 #pragma unroll
@@ -2372,7 +2419,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     int bc = 0, bi = DIST % NBUF;  // s % NBUF, (s + DIST) % NBUF
     // STEADY: stage s + DIST exists (one constant wait, an unconditional issue); the tail waits by
     // the count of stages still in flight (WO_SPLIT: two loops; else one loop with both tests)
-    auto step = [&](int s, auto steady_c) {
+    auto step = [&](int s, auto steady_c, auto nf_c) {
       constexpr bool STEADY = decltype(steady_c)::value;
       if constexpr ((WABL & WO_SPLIT) != 0) {
         if constexpr (STEADY) wait_vmcnt<(DIST - 1) * DPS>();
@@ -2409,17 +2456,20 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
           issue(s + DIST, bi);
         }
       }
-      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(bc);
+      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(bc, nf_c);
       bc = bc + 1 == NBUF ? 0 : bc + 1;
       bi = bi + 1 == NBUF ? 0 : bi + 1;
     };
-    if constexpr ((WABL & WO_SPLIT) != 0) {
-      int s = 0;
-      for (; s + DIST < nst; ++s) step(s, std::true_type());
-      for (; s < nst; ++s) step(s, std::false_type());
-    } else {
-      for (int s = 0; s < nst; ++s) step(s, std::true_type());
-    }
+    auto run = [&](auto nf_c) {
+      if constexpr ((WABL & WO_SPLIT) != 0) {
+        int s = 0;
+        for (; s + DIST < nst; ++s) step(s, std::true_type(), nf_c);
+        for (; s < nst; ++s) step(s, std::false_type(), nf_c);
+      } else {
+        for (int s = 0; s < nst; ++s) step(s, std::true_type(), nf_c);
+      }
+    };
+    run(std::integral_constant<int, FM>());
     wait_vmcnt<0>();
     lds_barrier();  // ring -> epilogue staging
   } else if (nst > 0) {
@@ -2440,7 +2490,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       gpos = gpos + 1 == gstages ? 0 : gpos + 1;
       if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
       if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
-      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF);
+      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF, std::integral_constant<int, FM>());
       if (next_group) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -2568,7 +2618,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
