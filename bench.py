@@ -133,7 +133,14 @@ def strong_scaling_step(cfg: str, dev, world: int, rank: int, steps: int, warmup
     inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down")) for gg in ("gate_up", "down")}
     stream = torch.cuda.current_stream(dev)
 
-    def timed(fn, k=steps, w=warmup):
+    def timed(fn, k=steps, w=warmup, settle=0.0):
+        # settle: seconds of untimed calls first — only for a collective-free fn (the count of calls
+        # may differ between ranks)
+        t_settle = time.perf_counter()
+        while time.perf_counter() - t_settle < settle:
+            for _ in range(4):
+                fn()
+            torch.cuda.synchronize(dev)
         for _ in range(w):
             fn()
         torch.cuda.synchronize(dev)
@@ -150,7 +157,7 @@ def strong_scaling_step(cfg: str, dev, world: int, rank: int, steps: int, warmup
         return float(t.item())
 
     full = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
-    t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)))
+    t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)), settle=settle_s)
     del full
     calls = {gg: ShardedCall(inp[gg], world, rank, variant=variant) for gg in inp}
     step = ShardedLayerStep(calls["gate_up"], calls["down"], overlap=True)
@@ -178,7 +185,7 @@ def _gather_only(step, stream) -> None:
 
 
 def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int, coll_dev, variant=None,
-                  median_iters: int = 50) -> dict:
+                  median_iters: int = 50, settle_s: float = 0.0) -> dict:
     """The N > 1 headline: ONE layer (the N = 1 workload) split by expert over the ranks
     (dist.EPLayerStep). Every rank holds the full inputs (same seeds), runs gate_up and down over its
     row items, and the packed down outputs are all-gathered over RCCL / xGMI. Timed K steps between
@@ -194,7 +201,14 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
     inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down")) for gg in ("gate_up", "down")}
     stream = torch.cuda.current_stream(dev)
 
-    def timed(fn, k=steps, w=warmup):
+    def timed(fn, k=steps, w=warmup, settle=0.0):
+        # settle: seconds of untimed calls first — only for a collective-free fn (the count of calls
+        # may differ between ranks)
+        t_settle = time.perf_counter()
+        while time.perf_counter() - t_settle < settle:
+            for _ in range(4):
+                fn()
+            torch.cuda.synchronize(dev)
         for _ in range(w):
             fn()
         torch.cuda.synchronize(dev)
@@ -211,7 +225,7 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
         return float(t.item())
 
     full = {gg: GroupGemm(inp[gg].problems, variant=variant, device=dev) for gg in inp}
-    t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)))
+    t1 = timed(lambda: (full["gate_up"].launch(stream), full["down"].launch(stream)), settle=settle_s)
     del full
     shared = CONFIGS[cfg].get("model") != "mixtral"
     step = EPLayerStep(inp["gate_up"], inp["down"], world, rank, variant=variant, shared=shared)
@@ -401,6 +415,10 @@ def main():
     # the chip needs ~0.2 s of sustained load to reach its steady clock: 10 warm-up steps read 3-5 %
     # low on the headline and 5-8 % on the extras (profiles/r02/verify2/warmup_ab.jsonl)
     ap.add_argument("--warmup", type=int, default=200)
+    # clock settle before the W warm-up steps: the timed steps then run at the steady clock whatever W
+    # the caller picks (round 3's driver run used W = 5: 0.398 of peak on the step clock against
+    # 0.436 on the kernels' own clock)
+    ap.add_argument("--settle-s", type=float, default=0.3, help="seconds of untimed steps before the warm-up")
     ap.add_argument("--config", default="fp16", choices=list(CONFIGS))
     ap.add_argument("--no-scaling-sim", action="store_true",
                     help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
@@ -468,6 +486,11 @@ def main():
             ggs["gate_up"].launch(stream)
             ggs["down"].launch(stream)
 
+        t_settle = time.perf_counter()
+        while time.perf_counter() - t_settle < args.settle_s:
+            for _ in range(4):
+                step()
+            torch.cuda.synchronize(dev)
         for _ in range(warmup):
             step()
         torch.cuda.synchronize(dev)
@@ -514,7 +537,7 @@ def main():
         # layer's FLOPs / max-rank time of compute + the RCCL all-gather of the layer's outputs
         vv = args.variant if args.variant >= 0 else None
         eres = ep_layer_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
-                             median_iters=args.median_iters)
+                             median_iters=args.median_iters, settle_s=args.settle_s)
         main_res = {"dt": eres["dt"], "total_flops": eres["total_flops"], "per": eres["per"],
                     "flops": eres["flops_local"], "variant": eres["variant"], "tiles": eres["tiles"],
                     "shapes": full_layer(cfg)}
@@ -657,6 +680,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_s": args.settle_s,
             "ms_per_step": round(main_res["dt"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",

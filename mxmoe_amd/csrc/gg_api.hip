@@ -707,8 +707,10 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       }
     }
     const double share = total / (kSplitCUs * v.chunk / 32);  // workgroup slots: CUs x workgroups per CU
+    const char* rmul_env = planner_knob("MXMOE_GG_SPLIT_RATIO_MUL");  // lab A/B: scale the ratio
+    const double rmul = rmul_env ? atof(rmul_env) : 1.0;
     for (int i : order) {
-      const double ratio = biggest[i] / std::max(share, 1.0);
+      const double ratio = rmul * biggest[i] / std::max(share, 1.0);
       // (w4a4 g128 never splits: summing f32 partial folds would change the rounding)
       if (ratio > 2.0 && all[i].qtype != QT_I4G) split[i] = std::max(1, std::min({8, (int)ratio, stages_of(all[i]) / 4}));
     }

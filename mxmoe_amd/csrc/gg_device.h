@@ -509,34 +509,36 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// Split-K hand-off (cdna_hip_programming.md §6 Guideline 16, counter form): every slice stores
-// its accumulators (thread-linear 16-B words: coalesced), drains, and one lane publishes with an
-// agent-scope release before the relaxed agent-scope ticket; the slice that draws nsplit - 1
-// acquires, re-zeroes the counter for the next launch and sums every slab in slice order.
-// Returns true when `acc` holds the complete K sum (not split, or the last slice).
+// Split-K hand-off (cdna_hip_programming.md §6 Guideline 16, counter form, write-through variant):
+// every slice stores its accumulators with sc1 buffer stores (thread-linear 16-B words: coalesced;
+// sc1 writes through the XCD's L2, so no agent-scope release — whose buffer_wbl2 wrote back every
+// dirty line of the XCD's L2, C tiles of other blocks included — is needed), drains, and one lane
+// takes the relaxed agent-scope ticket; the slice that draws nsplit - 1 re-zeroes the counter for
+// the next launch and sums every slab in slice order with sc1 loads (no acquire: its buffer_inv
+// emptied the XCD's L2 under the co-resident tiles' A / B panels). Returns true when `acc` holds
+// the complete K sum (not split, or the last slice).
 template <int NT, class Acc, int FM, int FN>
 __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& sk, uint8_t* lds,
                                               int tid = threadIdx.x) {
   if (sk.nsplit <= 1) return true;
   static_assert(FM * FN * NT * 16 <= SPLITK_SLAB_BYTES, "tile accumulators exceed one slab");
-  Acc* mine = reinterpret_cast<Acc*>(sk.slabs + (size_t)(sk.slab + sk.idx) * SPLITK_SLAB_BYTES);
+  static_assert(sizeof(Acc) == 16, "16-B accumulator words");
+  typedef unsigned int v4u_ __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t mine = __builtin_amdgcn_make_buffer_rsrc(
+      sk.slabs + (size_t)(sk.slab + sk.idx) * SPLITK_SLAB_BYTES, (short)0, SPLITK_SLAB_BYTES, 0x00020000);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) mine[(i * FN + j) * NT + tid] = acc[i][j];
+    for (int j = 0; j < FN; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_, acc[i][j]), mine, ((i * FN + j) * NT + tid) * 16, 0,
+                                             16 /* sc1 */);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int32_t* flag = reinterpret_cast<int32_t*>(lds);  // the ring is drained: LDS is free here
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(sk.counters + sk.grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == sk.nsplit - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(sk.counters + sk.grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (last) __hip_atomic_store(sk.counters + sk.grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = last;
   }
   __syncthreads();
@@ -548,11 +550,14 @@ __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = Acc{0, 0, 0, 0};
   for (int k = 0; k < sk.nsplit; ++k) {
-    const Acc* part = reinterpret_cast<const Acc*>(sk.slabs + (size_t)(sk.slab + k) * SPLITK_SLAB_BYTES);
+    const __amdgpu_buffer_rsrc_t part = __builtin_amdgcn_make_buffer_rsrc(
+        sk.slabs + (size_t)(sk.slab + k) * SPLITK_SLAB_BYTES, (short)0, SPLITK_SLAB_BYTES, 0x00020000);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] += part[(i * FN + j) * NT + tid];
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] += __builtin_bit_cast(
+            Acc, __builtin_amdgcn_raw_buffer_load_b128(part, ((i * FN + j) * NT + tid) * 16, 0, 16 /* sc1 */));
   }
   return true;
 }
