@@ -382,6 +382,7 @@ const std::vector<Variant>& variants() {
       // the small-batch weight-only tile: where its time goes (ablations: WRONG RESULTS by design)
       make_wo2<0, 3>("x_wo3_r3"),  // the round-3 loop
       make_wo2<kWo3, 3>("x_wo3"),
+      make_wo2<kWo3 | WO_ADEAD, 3>("x_wo3_adead"),
       make_wo2<kWo3 | V2_TRACE, 3>("abl_wo3_trace"),
       make_wo2<kWo3 | ABL_WO_NODMA, 3>("abl_wo3_nodma"),
       make_wo2<kWo3 | ABL_WO_NOCOMPUTE, 3>("abl_wo3_nocompute"),

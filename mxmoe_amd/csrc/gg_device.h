@@ -636,7 +636,10 @@ enum : int {
   // with WO_SCLATE: the steady state (stage s + DIST exists) and the tail as two loops
   WO_SPLIT = 8192,
   // weight-only option: 4 / 2-bit codes converted where they sit (WoK::nibpos)
-  WO_NIBPOS = INT32_MIN
+  WO_NIBPOS = INT32_MIN,
+  // with WO_SCLATE | WO_SPLIT: waves whose A rows all lie past M issue no A piece (gg_tile_wo;
+  // the bit is ABL_B_TILED's, an int8-only v2 ablation gg_tile_wo never sees)
+  WO_ADEAD = 2048
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -2114,6 +2117,12 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
         srcB[j] = B + (int64_t)(n0 / Cfg::BN) * (mt.K / 64) * (Cfg::BN * RB) + row * RB + chunk * GRAN;
     }
   }
+  // WO_ADEAD (64-row tiles: one A piece of 8 rows per wave): a wave whose 8 A rows all lie past M
+  // issues no A piece — those LDS rows feed only output rows that are never stored — and counts
+  // GBW pieces per stage in its waits
+  static_assert((WABL & WO_ADEAD) == 0 || ((WABL & WO_SPLIT) != 0 && (WABL & WO_SCLATE) != 0),
+                "the per-wave piece count is only honoured by the split WO_SCLATE loop");
+  const bool a_live = (WABL & WO_ADEAD) == 0 || GA != 1 || wave * 8 < M - m0;
   auto issue = [&](int s, int buf) {
     if constexpr ((WABL & ABL_WO_NODMA) != 0) {
       if (s >= NBUF) return;
@@ -2121,8 +2130,10 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     uint8_t* As = lds + buf * SB_;
     uint8_t* Bs = As + Cfg::A_BYTES;
     const int64_t boff = (WABL & ABL_WO_BTILED) ? (int64_t)(ks0 + s) * (Cfg::BN * RB) : (int64_t)(ks0 + s) * RB;
+    if (a_live) {
 #pragma unroll
-    for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
+      for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
+    }
 #pragma unroll
     for (int j = 0; j < GBW; ++j) {
       if constexpr (BITS == 2)
@@ -2242,15 +2253,17 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   };
 
   // wait until stage t's LDS-DMA (this wave's) has landed, `later` stages having been issued after it
-  auto wait_stage = [&](int later) {
-    if constexpr (DIST >= 7) if (later >= 6) { wait_vmcnt<6 * DPS>(); return; }
-    if constexpr (DIST >= 6) if (later == 5) { wait_vmcnt<5 * DPS>(); return; }
-    if constexpr (DIST >= 5) if (later == 4) { wait_vmcnt<4 * DPS>(); return; }
-    if constexpr (DIST >= 4) if (later == 3) { wait_vmcnt<3 * DPS>(); return; }
-    if constexpr (DIST >= 3) if (later == 2) { wait_vmcnt<2 * DPS>(); return; }
-    if constexpr (DIST >= 2) if (later == 1) { wait_vmcnt<DPS>(); return; }
+  auto wait_stage_n = [&](int later, auto dps_c) {  // DPS_: pieces per stage of this wave
+    constexpr int DPS_ = decltype(dps_c)::value;
+    if constexpr (DIST >= 7) if (later >= 6) { wait_vmcnt<6 * DPS_>(); return; }
+    if constexpr (DIST >= 6) if (later == 5) { wait_vmcnt<5 * DPS_>(); return; }
+    if constexpr (DIST >= 5) if (later == 4) { wait_vmcnt<4 * DPS_>(); return; }
+    if constexpr (DIST >= 4) if (later == 3) { wait_vmcnt<3 * DPS_>(); return; }
+    if constexpr (DIST >= 3) if (later == 2) { wait_vmcnt<2 * DPS_>(); return; }
+    if constexpr (DIST >= 2) if (later == 1) { wait_vmcnt<DPS_>(); return; }
     wait_vmcnt<0>();
   };
+  auto wait_stage = [&](int later) { wait_stage_n(later, std::integral_constant<int, DPS>()); };
   // WO_PIPE (128 / 64-row tiles, WM = 1: their fragment sets are small): the fragments of stage
   // s+1 are read into a second register set right after the barrier that publishes stage s+1,
   // and stage s's dequant + MFMAs (first set) run while those reads are in flight; the reads no
@@ -2426,7 +2439,15 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     // the count of stages still in flight (WO_SPLIT: two loops; else one loop with both tests)
     auto step = [&](int s, auto steady_c, auto nf_c) {
       constexpr bool STEADY = decltype(steady_c)::value;
-      if constexpr ((WABL & WO_SPLIT) != 0) {
+      if constexpr ((WABL & WO_SPLIT) != 0 && (WABL & WO_ADEAD) != 0) {
+        if (a_live) {
+          if constexpr (STEADY) wait_vmcnt<(DIST - 1) * DPS>();
+          else wait_stage(nst - 1 - s);
+        } else {
+          if constexpr (STEADY) wait_vmcnt<(DIST - 1) * (DPS - GA)>();
+          else wait_stage_n(nst - 1 - s, std::integral_constant<int, DPS - GA>());
+        }
+      } else if constexpr ((WABL & WO_SPLIT) != 0) {
         if constexpr (STEADY) wait_vmcnt<(DIST - 1) * DPS>();
         else wait_stage(nst - 1 - s);
       } else {
@@ -2623,7 +2644,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
