@@ -638,7 +638,8 @@ enum : int {
   // weight-only option: 4 / 2-bit codes converted where they sit (WoK::nibpos)
   WO_NIBPOS = INT32_MIN,
   // with WO_SCLATE | WO_SPLIT: waves whose A rows all lie past M issue no A piece (gg_tile_wo;
-  // the bit is ABL_B_TILED's, an int8-only v2 ablation gg_tile_wo never sees)
+  // the bit is ABL_B_TILED's, an int8-only v2 ablation gg_tile_wo never sees). MEASURED NEGATIVE
+  // (round 4, lab): 0.5-2.5 % slower on the bs 512 calls (profiles/r04/wo/wo_i)
   WO_ADEAD = 2048
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;

@@ -50,10 +50,11 @@ def test_cost_model_predicts_layer_calls():
         meas = {c: res[(c, g)][1] for c in ("fp16", "w8a8", "w4a4")}
         assert max(pred, key=pred.get) == max(meas, key=meas.get) == "fp16", (g, pred, meas)
         # w8a8 (v2x) and w4a4 (v3) run within a few % of each other since round 3: a measured gap
-        # under 5 % is a tie, which the model must then also predict as close (< 20 %: the table's
-        # v3 entries, measured on 4 x 4-tile problems, run up to ~16 % high on the layer's gate_up
-        # call — within the 25 % per-call bound above); a wider measured gap must be ranked the same way
+        # under 5 % is a tie, which the model must then also predict as close (< 15 %: the table's
+        # w4a4 row, re-measured in round 4 on 4 x 4-tile problems, still prices the layer's v3
+        # calls 10-13 % high — inside the 25 % per-call bound above); a wider measured gap must be
+        # ranked the same way
         if abs(meas["w8a8"] / meas["w4a4"] - 1) <= 0.05:
-            assert abs(pred["w8a8"] / pred["w4a4"] - 1) < 0.20, (g, pred, meas)
+            assert abs(pred["w8a8"] / pred["w4a4"] - 1) < 0.15, (g, pred, meas)
         else:
             assert (pred["w8a8"] < pred["w4a4"]) == (meas["w8a8"] < meas["w4a4"]), (g, pred, meas)
