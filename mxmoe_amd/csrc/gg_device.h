@@ -881,7 +881,15 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
   const int swz = (r16 >> 1) & 7;  // rows of a fragment are base + r16 with base % 16 == 0
   const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u;
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
+  // a wave whose rows all lie past M (the small-batch 64 x 128 tiles' 16-row waves on ~35-row
+  // experts) skips its fragment reads and MFMAs; its accumulators stay zero and are never stored
+#ifndef MXMOE_V2_NO_WSKIP
+  const bool wave_dead = m0 + wm * Cfg::WTM >= M;
+#else
+  const bool wave_dead = false;
+#endif
   auto compute = [&](int buf) {
+    if (wave_dead) return;
     const uint8_t* As = lds + buf * Cfg::STAGE_BYTES + a_row;
     const uint8_t* Bs = lds + buf * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
     if constexpr (QT == QT_F8) {

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--bs", type=int, default=8192)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--split", default="qtype", choices=["qtype", "shared"],
+                    help="shared: the largest-M problem (the shared expert) on v2x (variant 1) vs the rest on AUTO")
     args = ap.parse_args()
     for gg_name in ("gate_up", "down"):
         if args.cfg == "ds2_mixed":
@@ -43,10 +45,16 @@ def main():
             shapes = load_workload(qwen2_layer11_workload(args.bs, qconfig=mixed_qconfig_lp1()))["layer-11"][gg_name]
         inp = build_layer_inputs(shapes)
         probs = inp.problems
-        p8 = [p for p, s in zip(probs, shapes) if s.a_bits == 8]
-        p4 = [p for p, s in zip(probs, shapes) if s.a_bits == (16 if args.cfg == "w4a16_w8a8" else 4)]
+        if args.split == "shared":
+            big = max(range(len(shapes)), key=lambda i: shapes[i].M)
+            p8 = [probs[big]]
+            p4 = [p for i, p in enumerate(probs) if i != big]
+            g8, g4 = GroupGemm(p8, variant=1), GroupGemm(p4)
+        else:
+            p8 = [p for p, s in zip(probs, shapes) if s.a_bits == 8]
+            p4 = [p for p, s in zip(probs, shapes) if s.a_bits == (16 if args.cfg == "w4a16_w8a8" else 4)]
+            g8, g4 = GroupGemm(p8), GroupGemm(p4)
         fused = GroupGemm(probs)
-        g8, g4 = GroupGemm(p8), GroupGemm(p4)
         main_s = torch.cuda.current_stream()
         s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 
