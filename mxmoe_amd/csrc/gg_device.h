@@ -1120,7 +1120,17 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       lds_barrier();
       if constexpr (!B3) stash_scale();  // (B3: the rings fill the LDS, the stash follows the mainloop)
       uint64_t st_body = 0, st_vm = 0, st_bar = 0;
-      if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
+#ifndef MXMOE_V2_NO_LATEDEAD
+      // every row of the late waves lies past M (a tail tile of <= BM / 2 rows: the int paths'
+      // 128-row class holding <= 64): with EDMA they issue no DMA piece either, so they skip their
+      // fragment reads and MFMAs and only keep the barrier count (one per stage, as below)
+      const bool late_dead = EDMA && Cfg::WM % 2 == 0 && M - m0 <= Cfg::BM / 2;
+#else
+      const bool late_dead = false;
+#endif
+      if (wave >= Cfg::WM * Cfg::WN / 2 && late_dead) {
+        for (int s = 0; s < nst; ++s) lds_barrier();
+      } else if (wave >= Cfg::WM * Cfg::WN / 2) {  // late waves
         if constexpr ((ABL & V2_PRIO_LATE) != 0) __builtin_amdgcn_s_setprio(1);
         dma_generic(0, false);
         hread(fr, 0, 0);
