@@ -274,8 +274,8 @@ Variant make_v3(const char* name) {
   return v;
 }
 
-template <int ABL = 0>
-Variant make_v2(const char* name) {
+// the v2 family's geometry (launch set by the caller)
+Variant v2_base(const char* name, int lds_bytes) {
   Variant v;
   v.name = name;
   v.kind = Kind::V2;
@@ -285,11 +285,17 @@ Variant make_v2(const char* name) {
   v.geom[QT_W2A16] = {256, 256, 16, 512};  // 64-K stages: 16 B of 2-bit codes per row
   v.geom[QT_I4G] = {256, 256, 128, 512};  // w4a4 g128 (gg_tile_g128): 256 / 128-row classes as int4
   v.threads = 512;
-  v.lds_bytes = (ABL & V2_B3) ? 160 * 1024 : V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA;
+  v.lds_bytes = lds_bytes;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
   v.k_stage_bytes = 0;  // K tails handled in-kernel (last stage)
   v.tail_bm = 128;
   v.tail2_bm = 64;  // <= 64 remaining rows, fp16 / weight-only problems (small batches)
+  return v;
+}
+
+template <int ABL = 0>
+Variant make_v2(const char* name) {
+  Variant v = v2_base(name, (ABL & V2_B3) ? 160 * 1024 : V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA);
   v.launch = &launch_v2<ABL>;
   return v;
 }
@@ -300,7 +306,7 @@ bool is_weightonly(int qt);
 // wo2: weight-only problems only, 64-row tiles, NWG workgroups per CU (gg_wo2_kernel)
 template <int ABL = 0, int NWG = 2>
 Variant make_wo2(const char* name) {
-  Variant v = make_v2<ABL>(name);
+  Variant v = v2_base(name, wo2_lds_bytes<NWG>());  // (no v2 kernel instantiated for the wo flags)
   for (int q = 0; q < QT_COUNT; ++q)
     if (!is_weightonly(q)) v.geom[q] = {0, 0, 0, 0};
     else v.geom[q].bm = 64;

@@ -2221,8 +2221,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const uint32_t b_row = (uint32_t)(wn * Cfg::WTN + r16) * RB;
   // rows of a B fragment are base + r16 with base % 16 == 0, so the swizzle depends on r16 only
   const int bsw = (r16 >> RSH) & (LPR - 1);
-  auto compute = [&](int buf, auto nf_c) {  // NF: row blocks computed (FM)
-    constexpr int NF = decltype(nf_c)::value;
+  auto compute = [&](int buf) {
     const uint8_t* As = lds + buf * SB_ + a_row;
     const uint8_t* Bs = lds + buf * SB_ + Cfg::A_BYTES + b_row;
     uint32_t raw[FN][2];  // 4-bit: the codes of both K halves (one 8-B read); 8-bit: one K half
@@ -2456,7 +2455,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     int bc = 0, bi = DIST % NBUF;  // s % NBUF, (s + DIST) % NBUF
     // STEADY: stage s + DIST exists (one constant wait, an unconditional issue); the tail waits by
     // the count of stages still in flight (WO_SPLIT: two loops; else one loop with both tests)
-    auto step = [&](int s, auto steady_c, auto nf_c) {
+    auto step = [&](int s, auto steady_c) {
       constexpr bool STEADY = decltype(steady_c)::value;
       if constexpr ((WABL & WO_SPLIT) != 0 && (WABL & WO_ADEAD) != 0) {
         if (a_live) {
@@ -2501,20 +2500,17 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
           issue(s + DIST, bi);
         }
       }
-      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(bc, nf_c);
+      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(bc);
       bc = bc + 1 == NBUF ? 0 : bc + 1;
       bi = bi + 1 == NBUF ? 0 : bi + 1;
     };
-    auto run = [&](auto nf_c) {
-      if constexpr ((WABL & WO_SPLIT) != 0) {
-        int s = 0;
-        for (; s + DIST < nst; ++s) step(s, std::true_type(), nf_c);
-        for (; s < nst; ++s) step(s, std::false_type(), nf_c);
-      } else {
-        for (int s = 0; s < nst; ++s) step(s, std::true_type(), nf_c);
-      }
-    };
-    run(std::integral_constant<int, FM>());
+    if constexpr ((WABL & WO_SPLIT) != 0) {
+      int s = 0;
+      for (; s + DIST < nst; ++s) step(s, std::true_type());
+      for (; s < nst; ++s) step(s, std::false_type());
+    } else {
+      for (int s = 0; s < nst; ++s) step(s, std::true_type());
+    }
     wait_vmcnt<0>();
     lds_barrier();  // ring -> epilogue staging
   } else if (nst > 0) {
@@ -2535,7 +2531,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       gpos = gpos + 1 == gstages ? 0 : gpos + 1;
       if (next_group) load_scales((ks0 + s + 1) / gstages, s2n, z2n);  // lands under this stage's MFMAs
       if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
-      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF, std::integral_constant<int, FM>());
+      if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF);
       if (next_group) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
