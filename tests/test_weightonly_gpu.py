@@ -156,3 +156,20 @@ def test_w4a16_w8a8_layer_bs512_matches_oracle(bs, variant):
                 assert_f16_close(out, ref, h.K)
             else:
                 assert (out.view(np.uint16) == ref.view(np.uint16)).all(), f"{gg} w8a8 M={h.M}"
+
+
+@pytest.mark.parametrize("variant", WO)
+@pytest.mark.parametrize("bits", [2, 4, 8])
+def test_wo3_group_sizes_scale_slots_and_row_skip(bits, variant):
+    """wo3's round-4 loop (gg_tile_wo under kWo3): scale groups of 1 / 2 / 4 / 8 stages (g64 opens a
+    group at every stage: a scale DMA beside every ring buffer), sym and asym, experts of 1-63 rows
+    (row blocks past M skipped), a multi-m-tile problem, and a long-K low-fill call the planner
+    splits along K (scale groups crossing slice boundaries; write-through split-K hand-off)."""
+    specs = [(35, 512, 1024, 64, True), (17, 256, 2048, 64, False), (49, 768, 1536, 128, True),
+             (1, 256, 1024, 256, False), (63, 512, 2048, 512, True), (130, 264, 1024, 256, False),
+             (33, 256, 5632, 64, False), (64, 128, 4096, 128, True)]
+    hps = [HostProblem(M, N, K, QParams(16, bits, g, s), seed=900 + i, device=DEV)
+           for i, (M, N, K, g, s) in enumerate(specs)]
+    group_gemm([h.problem for h in hps], variant=variant)
+    torch.cuda.synchronize()
+    _check(hps)
