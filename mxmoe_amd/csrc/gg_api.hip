@@ -218,6 +218,7 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {  // fast lab build: the w4a16 and w4a16 + w8a8 sets only
     case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;
     case 10: launch_wo2_q<ABL, 10, NWG>(a, grid, s); break;
+    case 16: launch_wo2_q<ABL, 16, NWG>(a, grid, s); break;  // (lab: w8a16 at the variant's NWG)
     default:
       fprintf(stderr, "libmxmoe_gg_lab (fast): wo2 quant-type mix %#x not compiled\n", qmask);
       abort();
@@ -388,6 +389,7 @@ const std::vector<Variant>& variants() {
       // the small-batch weight-only tile: where its time goes (ablations: WRONG RESULTS by design)
       make_wo2<0, 3>("x_wo3_r3"),  // the round-3 loop
       make_wo2<kWo3, 3>("x_wo3"),
+      make_wo2<kWo3, 2>("x_wo2"),
       make_wo2<kWo3 | WO_ADEAD, 3>("x_wo3_adead"),
       make_wo2<kWo3 | V2_TRACE, 3>("abl_wo3_trace"),
       make_wo2<kWo3 | ABL_WO_NODMA, 3>("abl_wo3_nodma"),
