@@ -1025,31 +1025,6 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     }
   }
 #endif
-  // N halves for the small-batch weight-only kernel (lab knob MXMOE_GG_WO_NSPLIT=1): the tiles an
-  // XCD queue holds past its first round of workgroup slots run as two 64 x 128 tiles (class 1,
-  // gg_wo2_kernel), so the ragged second round is made of half-length work units (no K split,
-  // no partial sums)
-  const char* nsplit_env = planner_knob("MXMOE_GG_WO_NSPLIT");
-  if (v.lds_of && nsplit_env && nsplit_env[0] == '1') {
-    for (int x = 0; x < 8; ++x) {
-      std::vector<int>& q = queue[x];
-      if (q.size() <= (size_t)chunk) continue;
-      std::vector<int> q2(q.begin(), q.begin() + chunk);
-      for (size_t j = chunk; j < q.size(); ++j) {
-        const TileDesc td = all_tiles[q[j]];
-        const GGMeta& m = plan->meta[td.prob];
-        if (!is_weightonly(m.qtype) || (td.cls & 0xFF) != 0 || ((td.cls >> 16) & 0xFF) > 1 || td.n0 + 128 >= m.N) {
-          q2.push_back(q[j]);
-          continue;
-        }
-        for (int h = 0; h < 2; ++h) {
-          q2.push_back((int)all_tiles.size());
-          all_tiles.push_back(TileDesc{td.prob, td.m0, td.n0 + 128 * h, (td.cls & ~0xFF) | 1, td.ks0, td.ks1, td.slab, td.grp});
-        }
-      }
-      q.swap(q2);
-    }
-  }
   size_t qmax = 0;
   for (const auto& q : queue) qmax = std::max(qmax, q.size());
   int grid = 0;

@@ -1995,11 +1995,9 @@ __global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2
 // WM_ = waves along M: 2 for 256-row tiles; 1 for the 128 / 64-row classes, so that each B
 // fragment is dequantised by exactly one wave and reused over all its 4-8 A fragments (with 2 x 4
 // waves and 32-row wave tiles the dequant VALU outweighed the MFMAs 11:1 at small batch)
-// BN_ = 128 (wo3, the N halves of a call's second-round tiles): 8 waves of 64 x 16, the ring
-// sized with its per-stage 1-KiB scale slot (WO_SCLATE)
-template <int BM_, int WM_ = 2, int LDSB_ = V2Cfg<256>::LDS_BYTES, int BN_ = 256>
+template <int BM_, int WM_ = 2, int LDSB_ = V2Cfg<256>::LDS_BYTES>
 struct WoCfg {
-  static constexpr int BM = BM_, BN = BN_, NT = 512, KS = 64;  // KS: K elements per stage
+  static constexpr int BM = BM_, BN = 256, NT = 512, KS = 64;  // KS: K elements per stage
   static constexpr int WM = WM_, WN = 8 / WM_;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int FM = WTM / 16, FN = WTN / 16;
@@ -2013,8 +2011,7 @@ struct WoCfg {
   static constexpr int stage_bytes() { return A_BYTES + BN * KS * BITS / 8; }
   template <int BITS>
   static constexpr int nbuf() {
-    constexpr int per = stage_bytes<BITS>() + (BN_ != 256 ? 1024 : 0);
-    return LDSB_ / per > 8 ? 8 : LDSB_ / per;
+    return LDSB_ / stage_bytes<BITS>() > 8 ? 8 : LDSB_ / stage_bytes<BITS>();
   }
   static constexpr int LDSB = LDSB_;
   static_assert(2 * STAGE_BYTES <= LDSB_, "two stages must fit the LDS image");
@@ -2107,15 +2104,9 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   // B chunk swizzle: the 16-B chunk c of tile row n sits in LDS slot c ^ ((n >> RSH) & (LPR - 1)),
   // RSH = log2(rows per 256-B bank window); rows n, n + 256 / RB then hit different banks
   constexpr int RSH = BITS == 4 ? 3 : 2;
-  // B DMA wave-instructions per stage (whole tile) and per issuing wave: a 64 x 128 4-bit tile has
-  // 4, issued by waves 0-3 (the others count their A pieces only: WO_SCLATE | WO_SPLIT loop)
-  constexpr int GBT = Cfg::BN / RPI;
-  constexpr int GBW = GBT >= 8 ? GBT / 8 : 1;
-  static_assert(GBT >= 8 ? GBT % 8 == 0 : 8 % GBT == 0, "B pieces per stage");
-  static_assert(GBT >= 8 || ((WABL & WO_SPLIT) != 0 && (WABL & WO_SCLATE) != 0),
-                "a per-wave B piece count needs the split WO_SCLATE loop");
+  constexpr int GBW = Cfg::BN / RPI / 8;        // B DMA instructions per wave per stage
   constexpr int SB_ = Cfg::template stage_bytes<BITS>(), NBUF = Cfg::template nbuf<BITS>(), DIST = NBUF - 1;
-  constexpr int DPS = GA + GBW;  // LDS-DMA instructions per (issuing) wave per stage
+  constexpr int DPS = GA + GBW;  // LDS-DMA instructions per wave per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
@@ -2151,7 +2142,6 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   static_assert((WABL & WO_ADEAD) == 0 || ((WABL & WO_SPLIT) != 0 && (WABL & WO_SCLATE) != 0),
                 "the per-wave piece count is only honoured by the split WO_SCLATE loop");
   const bool a_live = (WABL & WO_ADEAD) == 0 || GA != 1 || wave * 8 < M - m0;
-  const bool b_issue = GBT >= 8 || wave < GBT;
   auto issue = [&](int s, int buf) {
     if constexpr ((WABL & ABL_WO_NODMA) != 0) {
       if (s >= NBUF) return;
@@ -2163,14 +2153,12 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
       for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
     }
-    if (b_issue) {
 #pragma unroll
-      for (int j = 0; j < GBW; ++j) {
-        if constexpr (BITS == 2)
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[j] + boff), (lds_void_t*)(Bs + (wave * GBW + j) * 256), 4, 0, 0);
-        else
-          glds16(srcB[j] + boff, Bs + (wave * GBW + j) * 1024);
-      }
+    for (int j = 0; j < GBW; ++j) {
+      if constexpr (BITS == 2)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[j] + boff), (lds_void_t*)(Bs + (wave * GBW + j) * 256), 4, 0, 0);
+      else
+        glds16(srcB[j] + boff, Bs + (wave * GBW + j) * 1024);
     }
   };
 
@@ -2469,17 +2457,17 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     // the count of stages still in flight (WO_SPLIT: two loops; else one loop with both tests)
     auto step = [&](int s, auto steady_c) {
       constexpr bool STEADY = decltype(steady_c)::value;
-      if constexpr ((WABL & WO_SPLIT) != 0) {
-        // this wave's pieces per stage: A unless WO_ADEAD drops them, B unless it issues none
-        auto go = [&](auto dps_c) {
-          constexpr int D = decltype(dps_c)::value;
-          if constexpr (STEADY) wait_vmcnt<(DIST - 1) * D>();
-          else wait_stage_n(nst - 1 - s, dps_c);
-        };
-        if (a_live && b_issue) go(std::integral_constant<int, GA + GBW>());
-        else if (a_live) go(std::integral_constant<int, GA>());
-        else if (b_issue) go(std::integral_constant<int, GBW>());
-        else go(std::integral_constant<int, 0>());
+      if constexpr ((WABL & WO_SPLIT) != 0 && (WABL & WO_ADEAD) != 0) {
+        if (a_live) {
+          if constexpr (STEADY) wait_vmcnt<(DIST - 1) * DPS>();
+          else wait_stage(nst - 1 - s);
+        } else {
+          if constexpr (STEADY) wait_vmcnt<(DIST - 1) * (DPS - GA)>();
+          else wait_stage_n(nst - 1 - s, std::integral_constant<int, DPS - GA>());
+        }
+      } else if constexpr ((WABL & WO_SPLIT) != 0) {
+        if constexpr (STEADY) wait_vmcnt<(DIST - 1) * DPS>();
+        else wait_stage(nst - 1 - s);
       } else {
         if (s + DIST - 1 < nst) wait_vmcnt<(DIST - 1) * DPS>();
         else wait_stage(nst - 1 - s);
@@ -2671,10 +2659,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  typedef WoCfg<64, 1, WO2_LDS_BYTES, 128> CfgN;  // class 1: an N half (second-round tiles)
   constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
-  constexpr bool kNHalf = (WP & WO_SCLATE) != 0 && (WP & WO_SPLIT) != 0;
-  const bool nhalf = kNHalf && (td.cls & 0xFF) == 1;
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
@@ -2688,28 +2673,9 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
     // w4a4 on the same 64 x 128 tile (two 24-KiB stages of 256 K, nibbles widened to int8 MFMA)
     const _Float16* SA = static_cast<const _Float16*>(args.ptr_SA[td.prob]);
     gg_tile_v2<V2Cfg<64, 128, 4, 2>, QT_I4, 0>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
-  } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) {
-    if constexpr (kNHalf) {
-      if (nhalf) gg_tile_wo<CfgN, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-      else gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    } else {
-      gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    }
-  } else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) {
-    if constexpr (kNHalf) {
-      if (nhalf) gg_tile_wo<CfgN, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-      else gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    } else {
-      gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    }
-  } else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) {
-    if constexpr (kNHalf) {
-      if (nhalf) gg_tile_wo<CfgN, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-      else gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    } else {
-      gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
-    }
-  }
+  } else if ((QM & (1 << QT_W4A16)) && mt.qtype == QT_W4A16) gg_tile_wo<Cfg, 4, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  else if ((QM & (1 << QT_W8A16)) && mt.qtype == QT_W8A16) gg_tile_wo<Cfg, 8, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
+  else if ((QM & (1 << QT_W2A16)) && mt.qtype == QT_W2A16) gg_tile_wo<Cfg, 2, WP>(mt, A, B, SB, C, td.m0, td.n0, lds, sk);
   if constexpr ((ABL & V2_TRACE) != 0) {  // (as gg_v2_kernel; the class field holds the problem index)
     if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) {
       wait_vmcnt<0>();
