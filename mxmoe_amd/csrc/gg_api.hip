@@ -390,6 +390,7 @@ const std::vector<Variant>& variants() {
       make_wo2<0, 3>("x_wo3_r3"),  // the round-3 loop
       make_wo2<kWo3, 3>("x_wo3"),
       make_wo2<kWo3, 2>("x_wo2"),
+      make_wo2<kWo3 | WO_BUF, 3>("x_wo3_buf"),
       make_wo2<kWo3 | WO_ADEAD, 3>("x_wo3_adead"),
       make_wo2<kWo3 | V2_TRACE, 3>("abl_wo3_trace"),
       make_wo2<kWo3 | ABL_WO_NODMA, 3>("abl_wo3_nodma"),

@@ -423,6 +423,13 @@ typedef const __attribute__((address_space(1))) void gbl_void_t;
 // so the MFMA loop needs no tail code and no extra registers).
 __device__ __attribute__((aligned(16))) const uint32_t g_zero16[4] = {0, 0, 0, 0};
 
+// buffer-form LDS-DMA pieces (resource in SGPRs, 32-bit lane offset, soffset)
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, uint32_t vo, int so) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 16, vo, so, 0, 0);
+}
+__device__ __forceinline__ void bdma4(__amdgpu_buffer_rsrc_t rs, uint8_t* lds_dst, uint32_t vo, int so) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_dst, 4, vo, so, 0, 0);
+}
 __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
@@ -640,7 +647,10 @@ enum : int {
   // with WO_SCLATE | WO_SPLIT: waves whose A rows all lie past M issue no A piece (gg_tile_wo;
   // the bit is ABL_B_TILED's, an int8-only v2 ablation gg_tile_wo never sees). MEASURED NEGATIVE
   // (round 4, lab): 0.5-2.5 % slower on the bs 512 calls (profiles/r04/wo/wo_i)
-  WO_ADEAD = 2048
+  WO_ADEAD = 2048,
+  // weight-only option: buffer-form LDS-DMA in gg_tile_wo (the bit is ABL_DMA_HOT's, a v2-only
+  // ablation gg_tile_wo never sees)
+  WO_BUF = 16
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
@@ -2142,6 +2152,18 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   static_assert((WABL & WO_ADEAD) == 0 || ((WABL & WO_SPLIT) != 0 && (WABL & WO_SCLATE) != 0),
                 "the per-wave piece count is only honoured by the split WO_SCLATE loop");
   const bool a_live = (WABL & WO_ADEAD) == 0 || GA != 1 || wave * 8 < M - m0;
+  // WO_BUF: buffer-form LDS-DMA (as v2x's V2_BUF): the tile's A / B bases in SGPR resources, a fixed
+  // 32-bit lane offset, the stage's K offset in soffset — no 64-bit address add per piece
+  constexpr bool kBuf = (WABL & WO_BUF) != 0 && (WABL & ABL_WO_BTILED) == 0;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(A) + (int64_t)m0 * lda, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B) + (int64_t)n0 * ldb, (short)0, 0x7fffffff, 0x00020000);
+  uint32_t voA[GA], voB[GBW];
+  if constexpr (kBuf) {
+#pragma unroll
+    for (int j = 0; j < GA; ++j) voA[j] = (uint32_t)(srcA[j] - (A + (int64_t)m0 * lda));
+#pragma unroll
+    for (int j = 0; j < GBW; ++j) voB[j] = (uint32_t)(srcB[j] - (B + (int64_t)n0 * ldb));
+  }
   auto issue = [&](int s, int buf) {
     if constexpr ((WABL & ABL_WO_NODMA) != 0) {
       if (s >= NBUF) return;
@@ -2151,11 +2173,20 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     const int64_t boff = (WABL & ABL_WO_BTILED) ? (int64_t)(ks0 + s) * (Cfg::BN * RB) : (int64_t)(ks0 + s) * RB;
     if (a_live) {
 #pragma unroll
-      for (int j = 0; j < GA; ++j) glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
+      for (int j = 0; j < GA; ++j) {
+        if constexpr (kBuf)
+          bdma16(rsA, As + (wave * GA + j) * 1024, voA[j], (ks0 + s) * 128);
+        else
+          glds16(srcA[j] + (ks0 + s) * 128, As + (wave * GA + j) * 1024);
+      }
     }
 #pragma unroll
     for (int j = 0; j < GBW; ++j) {
-      if constexpr (BITS == 2)
+      if constexpr (kBuf && BITS == 2)
+        bdma4(rsB, Bs + (wave * GBW + j) * 256, voB[j], (int)boff);
+      else if constexpr (kBuf)
+        bdma16(rsB, Bs + (wave * GBW + j) * 1024, voB[j], (int)boff);
+      else if constexpr (BITS == 2)
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(srcB[j] + boff), (lds_void_t*)(Bs + (wave * GBW + j) * 256), 4, 0, 0);
       else
         glds16(srcB[j] + boff, Bs + (wave * GBW + j) * 1024);
@@ -2659,7 +2690,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | WO_BUF | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
