@@ -630,10 +630,11 @@ enum : int {
   // store instruction): 13-15 % slower than the LDS-staged 8 rows x 128 B (probe: 5219 vs 2434 cycles
   // per tile), profiles/r04/lab_a/
   V2_PLAINST = 1 << 30,
-  // weight-only option (non-pipelined loop, wo3): the next group's scale words are kept raw and
-  // packed after the stage's MFMAs, so the compiler's wait before the packing leaves the ring's DMA
-  // in flight (packed right after the load it became vmcnt(0): the whole ring drained at every group
-  // boundary, every second stage at g128); the group index is a counter, not a division per boundary
+  // weight-only option (non-pipelined loop, wo3): a stage that opens a scale group brings the
+  // group's scale words by LDS-DMA into a slot beside its ring buffer, covered by the stage's own
+  // counted wait (round 3 loaded them into registers right before use: the compiler's vmcnt(0)
+  // drained the whole ring at every group boundary, every second stage at g128); group positions
+  // and ring indices are counters, not a division / modulo per stage
   WO_SCLATE = 32,
   // weight-only option: the code -> fp16 constants in registers (WoK): one v_and_or_b32 per fp16
   // pair (4 / 2-bit codes), one v_perm_b32 (8-bit) — VALU-bound small-batch tiles
