@@ -116,7 +116,7 @@ def full_layer(cfg: str, bs: int = 8192):
 
 
 def strong_scaling_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int, coll_dev, variant=None,
-                        median_iters: int = 50) -> dict:
+                        median_iters: int = 50, settle_s: float = 0.0) -> dict:
     """The N > 1 headline (SURVEY.md §8e, strong scaling): ONE layer (the N = 1 workload) split over
     the ranks by dist.nslice_plan. Every rank holds the full inputs (same seeds), runs its work list
     with its C slices packed into one local shard, and the shards are all-gathered over RCCL / xGMI;
@@ -575,7 +575,7 @@ def main():
         if args.dist_extras_all:
             try:  # the N-slice split: both calls' C all-gathered (gate_up gather beside down)
                 sres = strong_scaling_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
-                                           median_iters=10)
+                                           median_iters=10, settle_s=args.settle_s)
                 extras["strong_scaling_nslice"] = {
                     "what": "one layer split by dist.nslice_plan; step = compute + all-gather of every call's C "
                             "(gate_up gather on a second stream beside the down call), serial = without the overlap",
@@ -681,6 +681,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "settle_s": args.settle_s,
+            "materialise_after_plan": bool(args.materialise_after_plan),
             "ms_per_step": round(main_res["dt"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
@@ -690,8 +691,9 @@ def main():
                     "quantised problems; routed M_e = " + ("reference's committed bs=8192 histogram"
                                                          if not (cfg.startswith("ds2") or "model" in CONFIGS[cfg]) else
                                                          "seeded multinomial (SURVEY.md 8d)"),
-            "config": {"workload": CONFIGS[cfg]["name"] + (f", one layer split by expert over {world} GPUs (RCCL "
-                                                          f"all-gather of the layer outputs)" if world > 1 else ""),
+            "config": {"workload": CONFIGS[cfg]["name"] + (f", one layer split by expert over {world} GPUs "
+                                                          f"({'RCCL' if backend == 'nccl' else backend} all-gather "
+                                                          f"of the layer outputs)" if world > 1 else ""),
                        "model": {"mixtral": "Mixtral-8x7B", "qwen2_moe_57b": "Qwen2-57B-A14B"}.get(
                            CONFIGS[cfg].get("model"),
                            "DeepSeek-V2-Lite" if cfg.startswith("ds2") else "qwen2_moe (Qwen1.5-MoE-A2.7B)")

@@ -166,6 +166,11 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
  * rebound on the stream its launches run on: the upload is ordered behind that stream's work only. */
 int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const mxmoe_gg_plan_info* info, void* stream);
 
+/* Drop mxmoe_gg_rebind's remembered plan key for `workspace` (call before freeing a workspace that
+ * held a plan; host only, no device access). A later plan into the same address re-registers it.
+ * Returns MXMOE_GG_OK whether or not an entry existed. */
+int mxmoe_gg_forget_workspace(const void* workspace);
+
 /* Launch a planned GroupGEMM on `stream`. No allocation, no synchronisation. */
 int mxmoe_gg_launch(const mxmoe_gg_plan_info* info, void* stream);
 

@@ -78,7 +78,7 @@ class GGPlanInfo(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
-    "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_rebind", "mxmoe_gg_launch", "mxmoe_gg_run",
+    "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_rebind", "mxmoe_gg_forget_workspace", "mxmoe_gg_launch", "mxmoe_gg_run",
     "groupgemm_mxmoe", "groupgemm_mxmoe_fmt", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     "mxmoe_gg_plan_tiles",
     # include/mxmoe_moe.h (MoE-layer plumbing)
@@ -118,6 +118,8 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   c.POINTER(GGPlanInfo)]
     lib.mxmoe_gg_rebind.restype = c.c_int
     lib.mxmoe_gg_rebind.argtypes = [c.POINTER(GGProblemC), c.c_int, c.POINTER(GGPlanInfo), c.c_void_p]
+    lib.mxmoe_gg_forget_workspace.restype = c.c_int
+    lib.mxmoe_gg_forget_workspace.argtypes = [c.c_void_p]
     lib.mxmoe_gg_launch.restype = c.c_int
     lib.mxmoe_gg_launch.argtypes = [c.POINTER(GGPlanInfo), c.c_void_p]
     lib.mxmoe_gg_run.restype = c.c_int

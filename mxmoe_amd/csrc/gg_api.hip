@@ -25,7 +25,9 @@
 
 #include "../../include/mxmoe_gg.h"
 #include "gg_device.h"
-#include "gg_v2q.h"
+#ifdef MXMOE_LAB
+#include "gg_v2q.h"  // lab-only persistent kernel: not compiled into the product library
+#endif
 
 using namespace mxmoe;
 
@@ -181,6 +183,7 @@ void launch_v2p(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   }
 }
 
+#ifdef MXMOE_LAB
 template <int QM, int TRACE, int SAUX, int FILLALL>
 void launch_v2q_q(const GGArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((gg_v2q_kernel<QM, TRACE, SAUX, FILLALL>), dim3(grid), dim3(512), 0, s, a);
@@ -202,6 +205,8 @@ void launch_v2q(const GGArgs& a, int grid, int qmask, hipStream_t s) {
 #endif
   }
 }
+
+#endif  // MXMOE_LAB
 
 template <int ABL, int QM, int NWG>
 void launch_wo2_q(const GGArgs& a, int grid, hipStream_t s) {
@@ -332,6 +337,7 @@ Variant make_v2p(const char* name) {
   return v;
 }
 
+#ifdef MXMOE_LAB
 // v2q: the persistent v2x with the register epilogue and the next tile's ring fill before it
 // (gg_v2q.h); planned like v2p (per-workgroup tile lists)
 template <int TRACE = 0, int SAUX = 16, int FILLALL = 0>
@@ -341,6 +347,7 @@ Variant make_v2q(const char* name, int persist_len = 0) {
   v.persist_len = persist_len;
   return v;
 }
+#endif  // MXMOE_LAB
 
 // the small-batch weight-only tile's loop options (gg_tile_wo)
 constexpr int kWo3 = WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS;
@@ -1345,6 +1352,10 @@ static uint64_t rebind_key(const std::vector<HostProblem>& hp, int variant) {
       mix(v);
   return h;
 }
+// Invariant: every plan written into a workspace goes through mxmoe_gg_plan, which calls
+// remember_plan and so replaces the workspace's entry. An entry outlives its workspace only as a
+// stale key: a new workspace at the same address is planned (and re-remembered) before any rebind,
+// and mxmoe_gg_forget_workspace drops the entry when the caller frees the buffer.
 static void remember_plan(const void* ws, const std::vector<HostProblem>& hp, int variant, const Plan& plan) {
   std::lock_guard<std::mutex> lk(g_rebind_mu);
   if (g_rebind.size() >= 1024 && !g_rebind.count(ws)) g_rebind.clear();
@@ -1383,6 +1394,12 @@ int mxmoe_gg_plan(const mxmoe_gg_problem* problems, int problem_count, int varia
   return MXMOE_GG_OK;
 }
 
+int mxmoe_gg_forget_workspace(const void* workspace) {
+  std::lock_guard<std::mutex> lk(g_rebind_mu);
+  g_rebind.erase(workspace);
+  return MXMOE_GG_OK;
+}
+
 int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const mxmoe_gg_plan_info* info,
                     void* stream) {
   if (problem_count < 0 || (problem_count > 0 && !problems) || !info || !info->workspace)
@@ -1392,15 +1409,20 @@ int mxmoe_gg_rebind(const mxmoe_gg_problem* problems, int problem_count, const m
   const std::vector<HostProblem> hp = to_host(problems, problem_count);
   // fast path: the same shapes / quant params / strides as this workspace's plan -> only the
   // pointers are checked (build_meta's NULL / alignment checks), the tile planner is skipped
+  // (only a real key + signature hit takes it: an all-empty plan has an empty order too, and rebinding
+  // it with non-empty problems must go through the planner and fail the signature check)
   std::vector<int> order;
+  bool hit = false;
   {
     const uint64_t key = rebind_key(hp, info->variant);
     std::lock_guard<std::mutex> lk(g_rebind_mu);
     auto it = g_rebind.find(info->workspace);
-    if (it != g_rebind.end() && it->second.key == key && it->second.signature == info->signature)
+    if (it != g_rebind.end() && it->second.key == key && it->second.signature == info->signature) {
       order = it->second.order;
+      hit = true;
+    }
   }
-  if (!order.empty() || info->problem_count == 0) {
+  if (hit) {
     const Variant& v = variants()[info->variant];
     for (int i = 0; i < (int)hp.size(); ++i) {
       GGMeta m;

@@ -219,6 +219,15 @@ class GroupGemm:
         nat.check(nat.lib().mxmoe_gg_rebind(cps, P, ctypes.byref(self.info), ctypes.c_void_p(_stream_handle(stream))))
         self.problems, self._c_problems = problems, cps
 
+    def __del__(self):
+        # the workspace is freed with this object: drop the library's rebind key for its address
+        ws = getattr(self, "workspace", None)
+        if ws is not None and nat._lib is not None:
+            try:
+                nat._lib.mxmoe_gg_forget_workspace(ctypes.c_void_p(ws.data_ptr()))
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+
     def launch(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         nat.check(nat.lib().mxmoe_gg_launch(ctypes.byref(self.info), ctypes.c_void_p(_stream_handle(stream))))
 

@@ -13,6 +13,28 @@ QCFGS = {"fp16": FP16, "w8a8_g-1_sym": W8A8, "w4a4_g-1_sym": W4A4, "w4a4_g128_sy
          "w8a8_g-1_sym_E4M3": W8A8_E4M3, "bf16": BF16}
 
 
+FULL_SIZE_CFGS = ("fp16", "w8a8", "w4a4", "mixed", "ds2_mixed")  # BASELINE configs[1]-[4] at bs=8192
+
+
+def full_size_variants() -> list:
+    """Variants the full-size (bs=8192) parity tests run: EVERY production variant, so the kernel
+    AUTO hands a benched config to (the kernel of record) is always among them
+    (tests/test_abi.py::test_full_size_parity_covers_auto_choices guards this)."""
+    return list(nat.production_variants())
+
+
+def full_size_layer(cfg: str) -> dict:
+    """{"gate_up": [QShape], "down": [QShape]} of one BASELINE full-size config."""
+    from mxmoe_amd.workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1,
+                                    qwen2_layer11_workload)
+
+    if cfg == "ds2_mixed":
+        return load_workload(ds2_workload(8192, qconfig=ds2_mixed_qconfig()))["layer-1"]
+    kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
+          "mixed": dict(qconfig=mixed_qconfig_lp1())}[cfg]
+    return load_workload(qwen2_layer11_workload(8192, **kw))["layer-11"]
+
+
 def exact_compare(q: QParams) -> bool:
     """Integer-accumulating quant types are checked bit for bit; fp16 / bf16 / weight-only / E4M3
     (f32 sums in an unspecified order) within the fp16 tolerance."""

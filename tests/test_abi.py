@@ -194,6 +194,22 @@ def test_auto_variant_weightonly_small_batch_runs_wo3():
     assert wo3 in nat.production_variants() and wo3 in nat.production_variants("w4a16_g128_asym")
 
 
+def test_full_size_parity_covers_auto_choices():
+    """Guard: the full-size parity parametrisation must contain the default
+    variant and every variant AUTO resolves to on BASELINE configs[1]-[4], so a change to the
+    product table cannot silently drop the kernel the bench times from the bs=8192 oracle checks."""
+    from tests._util import FULL_SIZE_CFGS, full_size_layer, full_size_variants
+
+    covered = set(full_size_variants())
+    assert nat.default_variant() in covered
+    for cfg in FULL_SIZE_CFGS:
+        for gg, shapes in full_size_layer(cfg).items():
+            probs = [_prob(M=s.M, N=s.N, K=s.K, a_bits=s.a_bits, w_bits=s.w_bits, gsize=s.gsize, sym=int(s.sym),
+                           **({} if s.a_bits < 16 else dict(scale_a=0, scale_b=0))) for s in shapes]
+            v = nat.resolve_variant((nat.GGProblemC * len(probs))(*probs), len(probs))
+            assert v in covered, (cfg, gg, v)
+
+
 def _plan(problems, ws_bytes=1 << 20):
     arr = (nat.GGProblemC * len(problems))(*problems)
     info = nat.GGPlanInfo()

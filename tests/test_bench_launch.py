@@ -55,3 +55,35 @@ def test_bench_refuses_mismatched_world_size_before_gpu_work():
     r = subprocess.run([sys.executable, bench.__file__, "--gpus", "3"], env={"WORLD_SIZE": "2", "PATH": "/usr/bin"},
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "n_gpus must equal --gpus" in r.stderr
+
+
+def _unresolved_globals(path) -> set:
+    """Names a function in ``path`` reads as implicit globals that the module never binds and that are
+    not builtins (a pyflakes-style check via symtable: ADVICE r04 found `settle_s` read by
+    strong_scaling_step without being its parameter — a NameError swallowed by the extras' except)."""
+    import builtins
+    import symtable
+
+    top = symtable.symtable(open(path).read(), str(path), "exec")
+    bound = {s.get_name() for s in top.get_symbols() if s.is_assigned() or s.is_imported()} | {"__file__", "__name__"}
+    bad = set()
+
+    def walk(t):
+        for c in t.get_children():
+            if c.get_type() in ("function", "lambda"):
+                for s in c.get_symbols():
+                    if s.is_referenced() and s.is_global() and not s.is_declared_global():
+                        n = s.get_name()
+                        if n not in bound and not hasattr(builtins, n):
+                            bad.add(f"{c.get_name()}:{n}")
+            walk(c)
+
+    walk(top)
+    return bad
+
+
+def test_bench_functions_read_no_unbound_names():
+    assert _unresolved_globals(bench.__file__) == set()
+    import inspect
+
+    assert "settle_s" in inspect.signature(bench.strong_scaling_step).parameters

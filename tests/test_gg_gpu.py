@@ -7,6 +7,8 @@ K tails inside a 128-byte stage and strided C (N-slices) that the reference does
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -123,7 +125,7 @@ def test_unsupported_qtype_raises():
         group_gemm([p])
 
 
-@pytest.mark.parametrize("variant", [v for v in PROD if v >= 3] + [0])
+@pytest.mark.parametrize("variant", PROD)
 def test_graph_capture_replay(variant):
     hps = [HostProblem(150, 256, 512, W8A8, seed=31, device=DEV), HostProblem(90, 128, 256, W4A4, seed=32, device=DEV)]
     gg = GroupGemm([h.problem for h in hps], variant=variant)
@@ -300,3 +302,20 @@ def test_reference_abi_shim_plan_cache():
     b[0].problem.scale_a = None
     with pytest.raises(nat.GGError, match="NULL scale"):
         _shim_call(b)
+
+
+def test_rebind_all_empty_plan_rejects_non_empty_problems():
+    """a plan whose problems are all empty has an empty table order; rebinding it with
+    non-empty problems must fail the plan-signature check (not take the fast path and leave C
+    unwritten). The same empty shapes rebind fine; forgetting the workspace keeps that true."""
+    empty = [HostProblem(0, 128, 256, W8A8, seed=301, device=DEV), HostProblem(0, 256, 128, FP16, seed=302, device=DEV)]
+    gg = GroupGemm([h.problem for h in empty])
+    assert gg.total_tiles == 0
+    gg.rebind([h.problem for h in empty])  # same (empty) shapes: accepted
+    full = [HostProblem(64, 128, 256, W8A8, seed=303, device=DEV), HostProblem(32, 256, 128, FP16, seed=304, device=DEV)]
+    with pytest.raises(nat.GGError, match="differ from the planned call"):
+        gg.rebind([h.problem for h in full])
+    nat.check(nat.lib().mxmoe_gg_forget_workspace(ctypes.c_void_p(gg.workspace.data_ptr())))
+    gg.rebind([h.problem for h in empty])  # planner path after the key is dropped: still accepted
+    with pytest.raises(nat.GGError, match="differ from the planned call"):
+        gg.rebind([h.problem for h in full])

@@ -15,7 +15,7 @@ import torch
 from mxmoe_amd import _native as nat
 from mxmoe_amd.groupgemm import GroupGemm, Problem, QParams, group_gemm
 from oracle import oracle
-from tests._util import assert_f16_close
+from tests._util import FULL_SIZE_CFGS, assert_f16_close, full_size_layer, full_size_variants
 
 pytestmark = pytest.mark.gpu
 GOLD = Path(__file__).resolve().parent / "golden"
@@ -101,21 +101,15 @@ def _sample_check(inputs, n_rows=48, n_cols=48, seed=0):
             assert_f16_close(out, ref, p.K)
 
 
-@pytest.mark.parametrize("variant", [v for v in nat.production_variants() if v >= 3] + [0])
-@pytest.mark.parametrize("cfg", ["fp16", "w8a8", "w4a4", "mixed", "ds2_mixed"])
+@pytest.mark.parametrize("variant", full_size_variants())
+@pytest.mark.parametrize("cfg", FULL_SIZE_CFGS)
 def test_full_size_layer11_sampled_parity(cfg, variant):
     """BASELINE configs[1]-[4] at full size (bs=8192): qwen2_moe layer 11 fp16 / w8a8 / w4a4 / LP-1
-    mixed, and the DeepSeek-V2-Lite mixed w4a4+w8a8 layer (64 routed + 2 shared experts)."""
+    mixed, and the DeepSeek-V2-Lite mixed w4a4+w8a8 layer (64 routed + 2 shared experts), on every
+    production variant (v3, v2x — the benched AUTO kernel — and wo3)."""
     from mxmoe_amd.harness import build_layer_inputs
-    from mxmoe_amd.workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1,
-                                    qwen2_layer11_workload)
 
-    if cfg == "ds2_mixed":
-        wl = load_workload(ds2_workload(8192, qconfig=ds2_mixed_qconfig()))["layer-1"]
-    else:
-        kw = {"fp16": {}, "w8a8": dict(qstr="w8a8_g-1_sym"), "w4a4": dict(qstr="w4a4_g-1_sym"),
-              "mixed": dict(qconfig=mixed_qconfig_lp1())}[cfg]
-        wl = load_workload(qwen2_layer11_workload(8192, **kw))["layer-11"]
+    wl = full_size_layer(cfg)
     for gg in ("gate_up", "down"):
         inp = build_layer_inputs(wl[gg])
         ggm = GroupGemm(inp.problems, variant=variant)
