@@ -268,6 +268,50 @@ def ep_layer_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int,
             "tiles": {gg: g.total_tiles if g is not None else 0 for gg, g in gg_of.items()}}
 
 
+def ep_combine_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: int, coll_dev, variant=None) -> dict:
+    """The second N > 1 step (dist.EPCombineStep): the same expert split and compute as ep_layer_step,
+    then the token-owner exchange — routed down rows all-to-all'ed to their token's owner, combined
+    there in top-k order with its shared-expert rows (HIP mxmoe_moe_combine), the combined [T, H]
+    output all-gathered — instead of all-gathering every expert's down C. Synthetic routing consistent
+    with the workload's per-expert rows (dist.synthetic_routing)."""
+    import torch.distributed as dist
+
+    from mxmoe_amd.dist import EPCombineStep, synthetic_routing
+    from mxmoe_amd.harness import build_layer_inputs
+
+    layer = full_layer(cfg)
+    inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=42 + (gg == "down")) for gg in ("gate_up", "down")}
+    dn = layer["down"]
+    T = dn[-1].M
+    topk = -(-sum(s.M for s in dn[:-1]) // T)
+    step = EPCombineStep(inp["gate_up"], inp["down"], world, rank, synthetic_routing([s.M for s in dn[:-1]], T, topk))
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_comp = timed(lambda: step.compute(stream))
+    t_x = timed(lambda: step.exchange(stream))
+    t_step = timed(lambda: step(stream))
+    b = step.cplan.bytes_received(dn[0].N)
+    return {"t_compute": t_comp, "t_exchange": t_x, "dt": t_step, "topk": topk,
+            "a2a_MB_received_max": round(max(b["all_to_all"]) / 1e6, 1),
+            "allgather_out_MB_received": round(max(b["allgather_out"]) / 1e6, 1)}
+
+
 def cpu_info() -> dict:
     """Host CPU model and the threads the baseline may use (the GPU box exports OMP_NUM_THREADS=16:
     its share of a much larger machine, which os.cpu_count() would report)."""
@@ -558,6 +602,18 @@ def main():
             "speedup_compute": round(eres["t1"] / eres["t_compute"], 3),
             "speedup_with_allgather": round(eres["t1"] / eres["dt"], 3),
             "allgather_MB_received_per_rank": eres["allgather_MB_received_per_rank"]}
+        try:  # the token-owner exchange (combine before the exchange): VERDICT r04 item 6
+            cres = ep_combine_step(cfg, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv)
+            extras["strong_scaling"]["combine_exchange"] = {
+                "what": "same split and compute; routed down rows all_to_all_single'd to their token's owner (the "
+                        "rank holding that token's shared-expert rows), combined there (mxmoe_moe_combine, top-k "
+                        "order), the combined [T, hidden] output all-gathered (dist.EPCombineStep)",
+                "compute_ms": round(ms(cres["t_compute"]), 4), "exchange_ms": round(ms(cres["t_exchange"]), 4),
+                "step_ms": round(ms(cres["dt"]), 4), "speedup_with_exchange": round(eres["t1"] / cres["dt"], 3),
+                "a2a_MB_received_max": cres["a2a_MB_received_max"],
+                "allgather_out_MB_received": cres["allgather_out_MB_received"]}
+        except Exception as e:  # an extra must not lose the headline
+            extras["strong_scaling"]["combine_exchange"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         for x in [e for e in args.dist_extras.split(",") if e and e != cfg]:
             try:  # BASELINE configs[4]: DeepSeek-V2-Lite mixed w4a4+w8a8 split by expert over the node
                 xr = ep_layer_step(x, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,

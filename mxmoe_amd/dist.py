@@ -409,3 +409,306 @@ class EPLayerStep:
     def scatter(self, outputs: Sequence[torch.Tensor]) -> None:
         for cplan, (*_, gathered, pad) in zip(self.chunk_plans, self.parts):
             ep_scatter(self.shapes_dn, cplan, gathered, pad, outputs)
+
+
+# ------------------------------------------------------------------ combine before the exchange
+#
+# EPLayerStep all-gathers every rank's per-expert down C (the layer's 168 MB of expert outputs at
+# qwen2_moe bs 8192: each rank receives ~152 MB at N = 8). What the MoE layer's consumer needs is the
+# top-k weighted combine of those rows, [T, hidden] fp16 (33.5 MB). The token-owner exchange below
+# sends each routed output row only to the rank that owns its token (an all-to-all of ~1/N of the
+# rows), combines there in top-k order with the shared expert's rows that rank computed itself
+# (mxmoe_moe_combine: the oracle's fma order, so the result is bit-identical to one-GPU
+# MoEFFN.forward), and optionally all-gathers the combined [T, hidden] output.
+
+
+@dataclasses.dataclass
+class TokenRouting:
+    """Host routing of one layer: topk_ids int32 [T, topk] (-1 = a dropped choice: the workload rule
+    int(p * T * topk) leaves sum(M_e) a few slots short of T * topk) and weights float32 [T, topk]
+    (0 for a dropped choice)."""
+
+    topk_ids: "np.ndarray"
+    weights: "np.ndarray"
+    E: int
+
+    @property
+    def T(self) -> int:
+        return int(self.topk_ids.shape[0])
+
+    @property
+    def topk(self) -> int:
+        return int(self.topk_ids.shape[1])
+
+    def slots(self):
+        """The slot order of mxmoe_moe_route (stable sort by expert; dropped choices last):
+        (sorted_expert, perm_token, inv_slot, counts[E], first_slot[E])."""
+        import numpy as np
+
+        flat = self.topk_ids.reshape(-1).astype(np.int64)
+        key = np.where(flat < 0, self.E, flat)
+        order = np.argsort(key, kind="stable")
+        inv = np.empty_like(order)
+        inv[order] = np.arange(order.size)
+        counts = np.bincount(key, minlength=self.E + 1)[: self.E]
+        first = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        return key[order], order // self.topk, inv, counts, first
+
+
+def synthetic_routing(counts: Sequence[int], T: int, topk: int, seed: int = 0) -> TokenRouting:
+    """A routing of T tokens whose per-expert row counts are exactly ``counts`` (the workload's M_e):
+    expert e's id appears M_e times, the T * topk - sum(M_e) other choices are dropped (-1), all in a
+    seeded random order; weights are seeded positive f32 values normalised per token (0 if dropped)."""
+    import numpy as np
+
+    n = T * topk
+    ids = np.concatenate([np.full(int(c), e, dtype=np.int32) for e, c in enumerate(counts)] +
+                         [np.full(n - int(sum(counts)), -1, dtype=np.int32)])
+    if ids.size != n:
+        raise ValueError(f"sum of counts {sum(counts)} exceeds T * topk = {n}")
+    rng = np.random.default_rng(seed)
+    ids = ids[rng.permutation(n)].reshape(T, topk)
+    w = rng.random((T, topk), dtype=np.float32) + np.float32(0.05)
+    w = np.where(ids < 0, np.float32(0), w)
+    s = w.sum(axis=1, keepdims=True)
+    w = (w / np.where(s > 0, s, 1)).astype(np.float32)
+    return TokenRouting(ids, w, len(counts))
+
+
+@dataclasses.dataclass
+class CombinePlan:
+    """Who sends which down-output rows to whom (identical on every rank; numpy, host)."""
+
+    world: int
+    topk: int
+    token_range: list          # per rank (t0, t1): the tokens it owns (= its shared-expert rows)
+    shared_base: list          # per rank: first row of its shared-expert rows in its packed down shard (-1: none)
+    send_rows: list            # send_rows[s][d]: rank s's packed-shard rows for rank d, in send order
+    inv_local: list            # per rank d: int32 [n_d * topk] rows of d's receive buffer (R_d = a zero row)
+    weights_local: list        # per rank d: float32 [n_d, topk]
+    recv_rows: list            # per rank d: R_d rows received in all
+
+    def split_sizes(self, rank: int):
+        """(rows rank sends to each rank, rows it receives from each rank)."""
+        return ([len(self.send_rows[rank][d]) for d in range(self.world)],
+                [len(self.send_rows[s][rank]) for s in range(self.world)])
+
+    def bytes_received(self, H: int) -> dict:
+        """Per-rank bytes received (fp16 rows of H) by the all-to-all (rows from other ranks) and by
+        the all-gather of the combined output ([T, H] minus the rank's own tokens)."""
+        T = self.token_range[-1][1] if self.token_range else 0
+        a2a = [2 * H * sum(len(self.send_rows[s][d]) for s in range(self.world) if s != d) for d in range(self.world)]
+        pad = max((t1 - t0 for t0, t1 in self.token_range), default=0)
+        ag = [2 * H * (self.world - 1) * pad for _ in range(self.world)]
+        return {"all_to_all": a2a, "allgather_out": ag, "T": T}
+
+
+def ep_combine_plan(plan: list[list[RowItem]], down: Sequence[QShape], routing: TokenRouting,
+                    shared: bool = True) -> CombinePlan:
+    """The token-owner exchange of an ep_layer_plan: rank d owns the tokens of its shared-expert row
+    slice (or an even token split without a shared expert); every routed down-output row goes to the
+    owner of its token; the owner's receive buffer holds rows source by source, each source's rows in
+    its send order (work order, then row order), plus one zero row for dropped choices."""
+    import numpy as np
+
+    world = len(plan)
+    P = len(down)
+    E = P - 1 if shared else P
+    T, topk = routing.T, routing.topk
+    if routing.E != E:
+        raise ValueError(f"routing has {routing.E} experts, the layer {E}")
+    sorted_e, perm_token, inv, counts, first = routing.slots()
+    for e in range(E):
+        if int(counts[e]) != down[e].M:
+            raise ValueError(f"expert {e}: routing has {int(counts[e])} rows, the layer {down[e].M}")
+    if shared and down[-1].M != T:
+        raise ValueError("the shared expert's rows must be the T tokens")
+    # token ranges: the shared-expert slices (contiguous, in rank order), else an even split
+    rng_ = [(0, 0)] * world
+    base_sh = [-1] * world
+    if shared:
+        for r, items in enumerate(plan):
+            base = 0
+            for w in items:
+                if w.problem == P - 1:
+                    rng_[r] = (w.m0, w.m1)
+                    base_sh[r] = base
+                base += w.rows
+        lo = 0
+        for r in range(world):  # ranks without shared rows own an empty range at the boundary
+            if rng_[r][1] == rng_[r][0]:
+                rng_[r] = (lo, lo)
+            lo = rng_[r][1]
+    else:
+        rng_ = [(T * r // world, T * (r + 1) // world) for r in range(world)]
+    if rng_[0][0] != 0 or rng_[-1][1] != T or any(rng_[r][1] != rng_[r + 1][0] for r in range(world - 1)):
+        raise ValueError(f"token ranges {rng_} do not tile [0, {T})")
+    owner = np.empty(T, dtype=np.int64)
+    for r, (t0, t1) in enumerate(rng_):
+        owner[t0:t1] = r
+    # send lists and where each routed slot lands in its owner's receive buffer
+    send = [[None] * world for _ in range(world)]
+    slot_src = np.full(int(counts.sum()), -1, dtype=np.int64)
+    slot_idx = np.full(int(counts.sum()), -1, dtype=np.int64)
+    for s, items in enumerate(plan):
+        rows_s, slots_s = [], []
+        base = 0
+        for w in items:
+            if w.problem < E:
+                sl = first[w.problem] + np.arange(w.m0, w.m1)
+                rows_s.append(base + np.arange(w.rows))
+                slots_s.append(sl)
+            base += w.rows
+        rows_s = np.concatenate(rows_s) if rows_s else np.zeros(0, np.int64)
+        slots_s = np.concatenate(slots_s) if slots_s else np.zeros(0, np.int64)
+        dest = owner[perm_token[slots_s]] if slots_s.size else np.zeros(0, np.int64)
+        for d in range(world):
+            m = dest == d
+            send[s][d] = rows_s[m]
+            slot_src[slots_s[m]] = s
+            slot_idx[slots_s[m]] = np.arange(int(m.sum()))
+    inv_local, w_local, recv_rows = [], [], []
+    for d in range(world):
+        off = np.cumsum([0] + [len(send[s][d]) for s in range(world)])
+        R = int(off[-1])
+        t0, t1 = rng_[d]
+        sl = inv.reshape(T, topk)[t0:t1].reshape(-1)
+        routed = sl < slot_src.size
+        pos = np.full(sl.size, R, dtype=np.int64)  # dropped choices read the zero row
+        pos[routed] = off[slot_src[sl[routed]]] + slot_idx[sl[routed]]
+        inv_local.append(pos.astype(np.int32))
+        w_local.append(np.ascontiguousarray(routing.weights[t0:t1], dtype=np.float32))
+        recv_rows.append(R)
+    return CombinePlan(world, topk, rng_, base_sh, send, inv_local, w_local, recv_rows)
+
+
+def _all_to_all_rows(recv: torch.Tensor, send: torch.Tensor, out_splits, in_splits, group=None) -> None:
+    """all_to_all_single over rows (RCCL on the node; staged through host memory under gloo with CUDA
+    tensors, the one-GPU rehearsal)."""
+    import torch.distributed as dist
+
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_to_all_single(host, send.cpu(), out_splits, in_splits, group=group)
+        recv.copy_(host)
+    else:
+        dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
+
+
+class CombineExchange:
+    """This rank's side of the token-owner exchange (ep_combine_plan): gather the rows to send from
+    the packed down shard (one index_select), exchange them with one all_to_all_single, combine the
+    owned tokens (``combine_fn``, default the HIP mxmoe_moe_combine), and — with ``gather_output`` —
+    all-gather the combined [T, H] output so every rank holds it (padded to the largest token range)."""
+
+    def __init__(self, cplan: CombinePlan, rank: int, H: int, device, combine_fn=None, gather_output: bool = True,
+                 group=None):
+        self.cp, self.rank, self.H, self.group = cplan, rank, H, group
+        self.gather_output = gather_output
+        dev = torch.device(device)
+        import numpy as np
+
+        self.send_idx = torch.from_numpy(
+            np.concatenate([cplan.send_rows[rank][d] for d in range(cplan.world)]).astype(np.int64)).to(dev)
+        self.in_splits, self.out_splits = cplan.split_sizes(rank)
+        R = cplan.recv_rows[rank]
+        self.send = torch.empty(int(self.send_idx.numel()), H, dtype=torch.float16, device=dev)
+        self.recv = torch.zeros(R + 1, H, dtype=torch.float16, device=dev)  # last row: zero (dropped choices)
+        self.inv = torch.from_numpy(cplan.inv_local[rank]).to(dev)
+        self.w = torch.from_numpy(cplan.weights_local[rank]).to(dev)
+        t0, t1 = cplan.token_range[rank]
+        self.n = t1 - t0
+        self.pad = max(t1 - t0 for t0, t1 in cplan.token_range)
+        self.out = torch.empty(max(self.pad, 1), H, dtype=torch.float16, device=dev)
+        self.gathered = torch.empty(cplan.world * max(self.pad, 1), H, dtype=torch.float16, device=dev)
+        if combine_fn is None:
+            from .moe import combine_into
+
+            def combine_fn(out, y, inv, w, shared, topk):
+                combine_into(out, y, inv, w, shared, topk)
+        self.combine_fn = combine_fn
+
+    def __call__(self, local2d: torch.Tensor) -> None:
+        """local2d: this rank's packed down shard as [rows, H] (routed rows + its shared rows)."""
+        if self.send.shape[0]:
+            torch.index_select(local2d, 0, self.send_idx, out=self.send)
+        _all_to_all_rows(self.recv[: self.recv.shape[0] - 1], self.send, self.out_splits, self.in_splits, self.group)
+        sb = self.cp.shared_base[self.rank]
+        shared = local2d[sb:sb + self.n] if sb >= 0 else None
+        self.combine_fn(self.out[: self.n], self.recv, self.inv, self.w, shared, self.cp.topk)
+        if self.gather_output:
+            _all_gather(self.gathered.view(-1), self.out.view(-1), self.group)
+
+    def full_output(self) -> torch.Tensor:
+        """The combined [T, H] layer output from the all-gathered buffer (gather_output=True)."""
+        parts = [self.gathered[r * max(self.pad, 1): r * max(self.pad, 1) + (t1 - t0)]
+                 for r, (t0, t1) in enumerate(self.cp.token_range)]
+        return torch.cat(parts, 0)
+
+
+class EPCombineStep:
+    """The second N > 1 step: EPLayerStep's compute (gate_up + down over this rank's row items; one
+    chunk) followed by the token-owner exchange (CombineExchange) instead of the all-gather of every
+    expert's down C."""
+
+    def __init__(self, gate_up, down, world: int, rank: int, routing: TokenRouting, variant: Optional[int] = None,
+                 group=None, shared: bool = True, gather_output: bool = True):
+        self.ep = EPLayerStep(gate_up, down, world, rank, variant=variant, group=group, shared=shared, chunks=1)
+        H = down.shapes[0].N
+        if any(s.N != H for s in down.shapes):
+            raise ValueError("the down problems must share N (= hidden)")
+        self.cplan = ep_combine_plan(self.ep.plan, down.shapes, routing, shared)
+        self.local2d = self.ep.parts[0][2][: sum(w.rows for w in self.ep.plan[rank]) * H].view(-1, H)
+        self.xchg = CombineExchange(self.cplan, rank, H, self.local2d.device, gather_output=gather_output, group=group)
+        self.flops_local = self.ep.flops_local
+
+    def compute(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        self.ep.compute(stream)
+
+    def exchange(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        with torch.cuda.stream(stream) if stream is not None else _null():
+            self.xchg(self.local2d)
+
+    def __call__(self, stream: torch.cuda.Stream) -> None:
+        self.ep.compute(stream)
+        self.exchange(stream)
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+COMBINE_GBS = 6000.0  # mxmoe_moe_combine's measured streaming rate (DESIGN.md §4: 6.5 TB/s at bs 8192)
+
+
+def exchange_model(t_compute_ms: float, world: int, pad_elems: int, cplan: Optional[CombinePlan], H: int) -> dict:
+    """Modelled N > 1 step of both exchanges from a rank's compute time (all in ms; links as in
+    gather_ms_model):
+      allgather:   north_star's form — every rank's per-expert down C all-gathered (EPLayerStep),
+                   compute and gather pipelined in dist.choose_chunks chunks;
+      combine:     the token-owner exchange (EPCombineStep) — all-to-all of routed rows to their
+                   token's owner, the combine there, all-gather of the combined [T, H] output;
+      combine_sharded: the same without the final all-gather (the output stays token-sharded, the
+                   layout a data-parallel consumer of the layer reads)."""
+    tg = gather_ms_model(2.0 * pad_elems * (world - 1), world)
+    c = choose_chunks(t_compute_ms, tg)
+    lo, hi = sorted((t_compute_ms, tg))
+    out = {"allgather": {"MB_received": round(2.0 * pad_elems * (world - 1) / 1e6, 1), "gather_ms": round(tg, 4),
+                         "chunks": c, "step_ms": round(hi + lo / c + (c - 1) * CHUNK_OVERHEAD_MS, 4)}}
+    if cplan is not None:
+        b = cplan.bytes_received(H)
+        a2a = max(b["all_to_all"])
+        ag = max(b["allgather_out"])
+        n_max = max(t1 - t0 for t0, t1 in cplan.token_range)
+        t_a2a = gather_ms_model(a2a, world)
+        t_ag = gather_ms_model(ag, world)
+        t_comb = n_max * H * 2 * (cplan.topk + 2) / (COMBINE_GBS * 1e9) * 1e3
+        out["combine"] = {"a2a_MB_received": round(a2a / 1e6, 1), "allgather_out_MB_received": round(ag / 1e6, 1),
+                          "a2a_ms": round(t_a2a, 4), "combine_ms": round(t_comb, 4), "allgather_out_ms": round(t_ag, 4),
+                          "step_ms": round(t_compute_ms + t_a2a + t_comb + t_ag, 4)}
+        out["combine_sharded"] = {"step_ms": round(t_compute_ms + t_a2a + t_comb, 4)}
+    return out

@@ -170,7 +170,7 @@ def ep_scaling_sim(gate_up: LayerInputs, down: LayerInputs, worlds: Sequence[int
     headline's plan), measured on ONE GPU: every rank's gate_up + down calls over its row items are
     timed as their own calls (ranks are independent GPUs); T_G = max over ranks, speedup = T_1 / T_G.
     The all-gather of the down outputs that follows on a node is listed as MB received per rank."""
-    from .dist import ep_layer_plan, ep_shard_elems
+    from .dist import ep_combine_plan, ep_layer_plan, ep_shard_elems, exchange_model, synthetic_routing
 
     def t_pair(gu, dn):
         ggs = [GroupGemm(x, variant=variant) for x in (gu, dn) if x]
@@ -185,9 +185,17 @@ def ep_scaling_sim(gate_up: LayerInputs, down: LayerInputs, worlds: Sequence[int
                    for items in plan]
         tg = max(rank_ms)
         pad = max(ep_shard_elems(down.shapes, items) for items in plan)
+        H = down.shapes[0].N
+        cplan = None
+        if shared and all(s.N == H for s in down.shapes):  # the token-owner exchange (synthetic routing)
+            routing = synthetic_routing([s.M for s in down.shapes[:-1]], down.shapes[-1].M,
+                                        max(1, -(-sum(s.M for s in down.shapes[:-1]) // max(1, down.shapes[-1].M))))
+            cplan = ep_combine_plan(plan, down.shapes, routing)
+        model = exchange_model(tg, G, pad, cplan, H)
         out[str(G)] = {"t_ms_max_rank": round(tg, 4), "speedup": round(t1 / tg, 3),
                        "rank_ms": [round(x, 4) for x in rank_ms],
-                       "allgather_MB_per_rank": round(2 * pad * (G - 1) / 1e6, 1)}
+                       "allgather_MB_per_rank": round(2 * pad * (G - 1) / 1e6, 1),
+                       "modelled": {k: {**v, "speedup": round(t1 / v["step_ms"], 3)} for k, v in model.items()}}
     return out
 
 

@@ -210,6 +210,18 @@ def combine(y: torch.Tensor, r: Routing, weights: torch.Tensor, shared: Optional
     return out
 
 
+def combine_into(out: torch.Tensor, y: torch.Tensor, inv_slot: torch.Tensor, weights: torch.Tensor,
+                 shared: Optional[torch.Tensor], topk: int, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """combine() on preallocated device buffers (no allocation, one launch: graph-capturable):
+    out [T, H] fp16, y [R, H] fp16 rows, inv_slot int32 [T*topk] rows of y, weights f32 [T, topk],
+    shared fp16 [T, H] or None. dist.CombineExchange's token-owner combine."""
+    T, H = out.shape
+    if T == 0:
+        return
+    nat.check(nat.lib().mxmoe_moe_combine(_ptr(y), _ptr(inv_slot), _ptr(weights), _ptr(shared), None, T, topk, H,
+                                          _ptr(out), _stream(stream)))
+
+
 # ------------------------------------------------------------------ reference-named entry points
 
 def _qtags(qparams_per_exp, n: int) -> list[int]:

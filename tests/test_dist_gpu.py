@@ -143,3 +143,65 @@ def test_ep_layer_step_matches_full_call(cfg, chunks):
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert all(n > 0 for *_, n in res)
+
+
+def _combine_worker(rank, world, port, cfg, q):
+    """dist.EPCombineStep (the token-owner exchange) on the GPU: 2 ranks share the GPU (gloo); the
+    combined [T, H] layer output must equal one full down call + the HIP combine on one GPU."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import numpy as np
+
+        from mxmoe_amd.dist import EPCombineStep, synthetic_routing
+        from mxmoe_amd.groupgemm import GroupGemm
+        from mxmoe_amd.harness import build_layer_inputs
+        from mxmoe_amd.moe import combine_into
+        from mxmoe_amd.workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        kw = {"fp16": {}, "mixed": dict(qconfig=mixed_qconfig_lp1())}[cfg]
+        T = 1024
+        layer = load_workload(qwen2_layer11_workload(T, **kw))["layer-11"]
+        inp = {gg: build_layer_inputs(layer[gg], device=dev, seed=7 + (gg == "down")) for gg in ("gate_up", "down")}
+        routing = synthetic_routing([s.M for s in layer["down"][:-1]], T, 4, seed=5)
+        step = EPCombineStep(inp["gate_up"], inp["down"], world, rank, routing)
+        s = torch.cuda.current_stream(dev)
+        step(s)
+        torch.cuda.synchronize(dev)
+        got = step.xchg.full_output().clone()
+        # the reference on one GPU: full down call, then the combine over every routed row
+        GroupGemm(inp["down"].problems).launch(s)
+        H = layer["down"][0].N
+        y = torch.cat([p.C[: p.M] for p in inp["down"].problems[:-1]] + [torch.zeros(1, H, dtype=torch.float16, device=dev)])
+        _, _, inv, _, _ = routing.slots()
+        inv_t = torch.from_numpy(np.minimum(inv, y.shape[0] - 1).astype(np.int32)).to(dev)
+        w_t = torch.from_numpy(routing.weights).to(dev)
+        ref = torch.empty(T, H, dtype=torch.float16, device=dev)
+        combine_into(ref, y, inv_t, w_t, inp["down"].problems[-1].C[:T], 4, s)
+        torch.cuda.synchronize(dev)
+        a, b = got.cpu().numpy(), ref.cpu().numpy()
+        if cfg == "mixed":
+            ok = bool(np.array_equal(a.view(np.uint16), b.view(np.uint16)))
+        else:
+            ok = bool(np.allclose(a.astype(np.float64), b.astype(np.float64), rtol=2e-3, atol=2e-3))
+        q.put((rank, ok, step.xchg.n))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", ["mixed", "fp16"])
+def test_ep_combine_step_matches_one_gpu_layer(cfg):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_combine_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert sum(n for *_, n in res) == 1024
