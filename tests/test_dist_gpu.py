@@ -185,7 +185,13 @@ def _combine_worker(rank, world, port, cfg, q):
         if cfg == "mixed":
             ok = bool(np.array_equal(a.view(np.uint16), b.view(np.uint16)))
         else:
-            ok = bool(np.allclose(a.astype(np.float64), b.astype(np.float64), rtol=2e-3, atol=2e-3))
+            # fp16: the one-GPU call and the per-rank calls may run different kernels (AUTO picks by
+            # the call's mean rows), whose f32 sums round differently; the combine then adds up to
+            # topk + 1 such rows, so the bar is relative to the output's rms (cancellation)
+            a64, b64 = a.astype(np.float64), b.astype(np.float64)
+            rms = float(np.sqrt(np.mean(b64 * b64)))
+            ok = bool(np.isfinite(a64).all() and (np.abs(a64 - b64) <= 2e-3 * np.abs(b64) + 2e-3 * rms).all()
+                      and np.linalg.norm(a64 - b64) <= 1e-3 * np.linalg.norm(b64))
         q.put((rank, ok, step.xchg.n))
     finally:
         dist.destroy_process_group()
