@@ -386,6 +386,7 @@ const std::vector<Variant>& variants() {
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
       // experiments under test only, fp16 / w8a8 bodies only
       make_v2<kV2x>("x_v2x"),
+      make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),
       make_v2q("x_v2q"),
@@ -408,6 +409,8 @@ const std::vector<Variant>& variants() {
       make_v0<T128x256, T128x256, T128x256>("v0_128x256_w4"),
       make_v2("v2_256x256_w8_dma"),
       make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
+      make_v2<kV2x>("x_v2x"),
+      make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
       make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),

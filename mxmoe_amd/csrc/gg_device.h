@@ -630,6 +630,10 @@ enum : int {
   // store instruction): 13-15 % slower than the LDS-staged 8 rows x 128 B (probe: 5219 vs 2434 cycles
   // per tile), profiles/r04/lab_a/
   V2_PLAINST = 1 << 30,
+  // int4 option (lab): an empty asm statement between the staggered loop's 8-B fragment reads, so
+  // hipcc cannot pair them into ds_read2st64_b64 (2-way bank conflicts on every pair; the bit is
+  // WO_SCLATE's, a gg_tile_wo option the v2 int4 body never sees)
+  V2_I4NOPAIR = 32,
   // weight-only option (non-pipelined loop, wo3): a stage that opens a scale group brings the
   // group's scale words by LDS-DMA into a slot beside its ring buffer, covered by the stage's own
   // counted wait (round 3 loaded them into registers right before use: the compiler's vmcnt(0)
@@ -695,6 +699,9 @@ __device__ __forceinline__ void v2_dma(const uint8_t* const (&src)[G], uint8_t* 
 
 template <class Cfg, int QT, int ABL = 0>
 struct V2Half {
+  // int4: 8-B reads per MFMA K step (hipcc pairs them into ds_read2st64_b64, 2-way bank conflicts:
+  // the 16-B form of gg_tile_v3 / the plain v2 loop adds the registers of the second step's words to
+  // the staggered loop, which sits at 254 VGPRs, and spilled there — DESIGN.md §7 round 5)
   typedef typename std::conditional<QT == QT_I4, v2i, v4i>::type word_t;
   static constexpr int FM = Cfg::FM, FN = Cfg::FN;
   static constexpr int SUBH = (QT == QT_I4) ? 2 : 1;  // MFMA K steps per 64-B half stage
@@ -711,9 +718,15 @@ struct V2Half {
       const uint32_t off = QT == QT_I4 ? (uint32_t)(((2 * (2 * h + t) + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8)
                                        : (uint32_t)(((h * 4 + g) ^ swz) << 4);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[t][i] = *reinterpret_cast<const word_t*>(As + i * 2048 + off);
+      for (int i = 0; i < FM; ++i) {
+        a[t][i] = *reinterpret_cast<const word_t*>(As + i * 2048 + off);
+        if constexpr (QT == QT_I4 && (ABL & V2_I4NOPAIR) != 0) asm volatile("");
+      }
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[t][j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
+      for (int j = 0; j < FN; ++j) {
+        b[t][j] = *reinterpret_cast<const word_t*>(Bs + j * 2048 + off);
+        if constexpr (QT == QT_I4 && (ABL & V2_I4NOPAIR) != 0) asm volatile("");
+      }
     }
   }
   __device__ __forceinline__ void mma(typename AccT<QT>::type (&acc)[FM][FN]) const {
@@ -919,18 +932,28 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma_f8_k128(b[j], a, acc[i][j]);
       }
     } else if constexpr (QT == QT_I4) {
+      // two 64-B halves; lane group g reads chunk (4 kc + g) ^ swz (16 B, as the int8 path) and
+      // runs two MFMA K steps on its 8-B halves (V2Half: the same K map for A and B)
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ swz) << 4) + (uint32_t)((g & 1) * 8);
+      for (int kc = 0; kc < 2; ++kc) {
+        const uint32_t off = (uint32_t)(((kc * 4 + g) ^ swz) << 4);
         v4i a[FM], b[FN];
 #pragma unroll
-        for (int i = 0; i < FM; ++i) a[i] = widen_i4(*reinterpret_cast<const v2i*>(As + i * 2048 + off));
+        for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const v4i*>(As + i * 2048 + off);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 2048 + off));
+        for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const v4i*>(Bs + j * 2048 + off);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int t = 0; t < 2; ++t) {
+          v4i bw[FN];
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) bw[j] = widen_i4(v2i{b[j][2 * t], b[j][2 * t + 1]});
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const v4i aw = widen_i4(v2i{a[i][2 * t], a[i][2 * t + 1]});
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bw[j], aw, acc[i][j], 0, 0, 0);
+          }
+        }
       }
     } else {
 #pragma unroll
@@ -1837,15 +1860,23 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
     const uint8_t* As = lds + (s % Cfg::NBUF) * Cfg::STAGE_BYTES + a_row;
     const uint8_t* Bs = lds + (s % Cfg::NBUF) * Cfg::STAGE_BYTES + Cfg::A_BYTES + b_row;
     if constexpr (QT == QT_I4) {
+      // lane group g reads chunk g ^ sw of the 64-B row (16 B = 32 nibbles, ds_read_b128 as the int8
+      // path: conflict-free under T) and runs two MFMA K steps on its 8-B halves; the same K map for
+      // A and B (V2Half). Round 4 read 8 B per step, paired by hipcc into ds_read2st64_b64: PMC had
+      // SQ_LDS_BANK_CONFLICT at 49 % of SQ_LDS_IDX_ACTIVE on the w4a4 layer
+      const uint32_t off = (uint32_t)((g ^ sw) << 4);
+      v4i braw[FN];
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {  // 2 x 32 bytes (= 64 int4) per 64-B stage
-        const uint32_t off = (uint32_t)(((2 * st + (g >> 1)) ^ sw) << 4) + (uint32_t)((g & 1) * 8);
-        v4i b[FN];  // B widened once, A per fragment row: 4 live widened registers instead of 4*FM
+      for (int j = 0; j < FN; ++j) braw[j] = *reinterpret_cast<const v4i*>(Bs + j * 1024 + off);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) b[j] = widen_i4(*reinterpret_cast<const v2i*>(Bs + j * 1024 + off));
+      for (int st = 0; st < 2; ++st) {
+        v4i b[FN];  // B widened once per step, A per fragment row
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = widen_i4(v2i{braw[j][2 * st], braw[j][2 * st + 1]});
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const v4i a = widen_i4(*reinterpret_cast<const v2i*>(As + i * 1024 + off));
+          const v4i araw = *reinterpret_cast<const v4i*>(As + i * 1024 + off);
+          const v4i a = widen_i4(v2i{araw[2 * st], araw[2 * st + 1]});
 #pragma unroll
           for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a, acc[i][j], 0, 0, 0);
         }
