@@ -375,7 +375,10 @@ const std::vector<Variant>& variants() {
       // tiles) — profiles/r03/lab/
       // (+ the weight-only tiles' pipelined fragment reads and, at 64 rows, the late-wave deferral:
       // +1-4 % on the small-batch w4a16 calls, profiles/r03/wo/)
-      make_v2<kV2x | WO_PIPE | WO_STAG>("v2x_256x256_w8_b3_buf_spread_edma"),
+      // round 5: int4 fragment reads kept unpaired (V2_I4NOPAIR: ds_read_b64 instead of 2-way-conflicted
+      // ds_read2st64_b64; lab A/B mixed gate_up / down -3.1 / -1.5 %, ds2_mixed -2.1 / -1.9 %,
+      // w4a4 on v2x -7.5 / -5.1 %: profiles/r05/nopair/)
+      make_v2<kV2x | WO_PIPE | WO_STAG | V2_I4NOPAIR>("v2x_256x256_w8_b3_buf_spread_edma"),
       // round 3 (AUTO for small-batch weight-only calls): the 64-row weight-only tile at three
       // workgroups per CU (gg_wo2_kernel<.., 3>; weight-only problems only) — profiles/r03/wo2/;
       // round 4: scale groups by LDS-DMA, register constants for the code -> fp16 step, codes
@@ -768,6 +771,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // m-tiles per band (n-major inside a band): a 32-tile chunk is band x (32 / band) tiles
   const char* band_env = planner_knob("MXMOE_GG_BAND");  // A/B switch (default 4)
   const size_t band = band_env && atoi(band_env) > 0 ? (size_t)atoi(band_env) : 4;
+  const char* ngroup_env = planner_knob("MXMOE_GG_NGROUP");  // A/B switch (default 1)
+  const int ngroup = ngroup_env && atoi(ngroup_env) > 0 ? atoi(ngroup_env) : 1;
   plan->meta.clear();
   plan->order = order;
   plan->slabs = 0;
@@ -858,9 +863,12 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       plan->meta.push_back(m);
       continue;
     }
+    // (lab A/B, MXMOE_GG_NGROUP = G: inside a band, n-tiles in groups of G, m-major inside a group —
+    // G = 1 is the default n-major order, G >= tiles_n m-major)
     for (size_t mb = 0; mb < mt.size(); mb += band)
-      for (int n = 0; n < nt; ++n)
-        for (size_t mi = mb; mi < std::min(mt.size(), mb + band); ++mi) {
+      for (int ng = 0; ng < nt; ng += ngroup)
+        for (size_t mi = mb; mi < std::min(mt.size(), mb + band); ++mi)
+          for (int n = ng; n < std::min(nt, ng + ngroup); ++n) {
           if (S == 1) {
             seq.push_back(TileDesc{row, mt[mi].first, n * g.bn, mt[mi].second, 0, nst, -1, -1});
             continue;

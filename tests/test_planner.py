@@ -128,7 +128,7 @@ def test_shared_expert_one_rectangle_per_xcd():
 
 
 KNOBS = {"MXMOE_GG_BAND": "8", "MXMOE_GG_REGION": "1", "MXMOE_GG_REGION_ROT": "1", "MXMOE_GG_ALIGN": "0",
-         "MXMOE_GG_TAIL_CHUNK": "4", "MXMOE_GG_XCD_RR": "1"}
+         "MXMOE_GG_TAIL_CHUNK": "4", "MXMOE_GG_XCD_RR": "1", "MXMOE_GG_NGROUP": "4"}
 
 
 @pytest.mark.parametrize("cfg", ["fp16", "w8a8"])
