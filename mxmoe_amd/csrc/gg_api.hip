@@ -414,6 +414,7 @@ const std::vector<Variant>& variants() {
       make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
       make_v2<kV2x>("x_v2x"),
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
+      make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
       make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
       make_v2<V2_STAGGER>("v2s_256x256_w8_dma_stagger"),
