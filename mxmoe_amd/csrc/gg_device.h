@@ -524,6 +524,12 @@ __device__ __forceinline__ void lds_barrier() {
 // the next launch and sums every slab in slice order with sc1 loads (no acquire: its buffer_inv
 // emptied the XCD's L2 under the co-resident tiles' A / B panels). Returns true when `acc` holds
 // the complete K sum (not split, or the last slice).
+// Invariant: the slab stores and the reducing loads both carry SPLITK_AUX (sc1). The slices of one
+// group may run on different XCDs (the planner's 16-entry tail chunks cut 5- and 8-slice groups;
+// tests/test_planner.py::test_tail_chunks_scatter_split_slices_across_xcds pins such plans and
+// tests/test_gg_gpu.py::test_splitk_slices_on_different_xcds runs them): a plain store would leave
+// the partials dirty in the writer's L2, a plain load could hit a stale line in the reader's.
+constexpr int SPLITK_AUX = 16;  // sc1 on both sides of the hand-off; never change one alone
 template <int NT, class Acc, int FM, int FN>
 __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& sk, uint8_t* lds,
                                               int tid = threadIdx.x) {
@@ -538,7 +544,7 @@ __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& 
 #pragma unroll
     for (int j = 0; j < FN; ++j)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_, acc[i][j]), mine, ((i * FN + j) * NT + tid) * 16, 0,
-                                             16 /* sc1 */);
+                                             SPLITK_AUX);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int32_t* flag = reinterpret_cast<int32_t*>(lds);  // the ring is drained: LDS is free here
@@ -564,7 +570,7 @@ __device__ __forceinline__ bool splitk_reduce(Acc (&acc)[FM][FN], const SplitK& 
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         acc[i][j] += __builtin_bit_cast(
-            Acc, __builtin_amdgcn_raw_buffer_load_b128(part, ((i * FN + j) * NT + tid) * 16, 0, 16 /* sc1 */));
+            Acc, __builtin_amdgcn_raw_buffer_load_b128(part, ((i * FN + j) * NT + tid) * 16, 0, SPLITK_AUX));
   }
   return true;
 }

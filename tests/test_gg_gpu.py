@@ -193,6 +193,27 @@ def test_splitk_long_k_low_fill(q, variant):
         assert torch.equal(h.problem.C.view(torch.int16), c.view(torch.int16))
 
 
+@pytest.mark.parametrize("q,K", [(W8A8, 4224), (W4A4, 4224), (FP16, 1408), (QParams(16, 4, 128, False), 1408)],
+                         ids=["w8a8", "w4a4", "fp16", "w4a16g128"])
+def test_splitk_slices_on_different_xcds(q, K):
+    """Split groups whose slices land on different XCDs (blockIdx % 8 differs, so different L2s):
+    the partial slabs are written with L2-bypassing stores and the arrival counter is a device-scope
+    atomic, so the last slice must still read every other slice's partials. The planner check in
+    tests/test_planner.py pins that these shapes do scatter slices across XCDs."""
+    from tests.test_planner import cross_xcd_split_groups
+
+    hps = [HostProblem(128, 2048, K, q, seed=140, device=DEV), HostProblem(40, 256, 1408, q, seed=141, device=DEV)]
+    gg = GroupGemm([h.problem for h in hps])
+    tiles, _ = nat.plan_tiles([h.problem.to_c() for h in hps], gg.variant)
+    assert cross_xcd_split_groups(tiles) > 0
+    for _ in range(2):  # second launch: counters were reset by the first
+        for h in hps:
+            h.problem.C.fill_(float("nan"))
+        gg.launch()
+        torch.cuda.synchronize()
+        _check(hps)
+
+
 @pytest.mark.parametrize("q", [FP16, W8A8], ids=["fp16", "w8a8"])
 def test_64bit_offsets_large_c(q):
     """C of 65536 x 33024 (2.16e9 elements > 2^31): row offsets into C (and A) need 64-bit address

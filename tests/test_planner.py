@@ -168,3 +168,24 @@ def test_routed_experts_stay_on_one_xcd():
     # purpose, to even out the XCDs' finish; every expert before them stays whole
     assert on_one >= 40, f"{on_one} of {len(routed)} routed experts on one XCD"
     assert all(len(homes[i]) <= 3 for i in routed)
+
+
+def cross_xcd_split_groups(tiles) -> int:
+    """Split-K groups whose slices sit on more than one XCD queue (blockIdx % 8)."""
+    homes = collections.defaultdict(set)
+    for b, t in enumerate(tiles):
+        if t[0] >= 0 and t[7] >= 0:
+            homes[int(t[7])].add(b % 8)
+    return sum(len(x) > 1 for x in homes.values())
+
+
+@pytest.mark.parametrize("wa,K", [((8, 8), 4224), ((4, 4), 4224), ((16, 16), 1408)], ids=["w8a8", "w4a4", "fp16"])
+def test_tail_chunks_scatter_split_slices_across_xcds(wa, K):
+    """A split group with 5 or 8 slices straddles the 16-entry tail chunks, so its slices land on
+    different XCDs (different L2s). tests/test_gg_gpu.py::test_splitk_slices_on_different_xcds runs
+    these shapes on the GPU; this pins that they keep exercising the cross-L2 hand-off."""
+    from mxmoe_amd.workload import QShape
+
+    shapes = [QShape([128, 2048, K], *wa), QShape([40, 256, 1408], *wa)]
+    tiles, _, _ = check_coverage(shapes)
+    assert cross_xcd_split_groups(tiles) > 0
