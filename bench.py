@@ -591,7 +591,7 @@ def main():
         extras["strong_scaling"] = {
             "what": "one layer split by expert (dist.ep_layer_plan: routed experts by index, shared expert by token "
                     "rows); T1 = the whole layer on one GPU (max over ranks), compute = max-rank time of the local "
-                    "gate_up + down calls, gather = the RCCL all_gather_into_tensor of the packed down outputs "
+                    "gate_up + down calls, gather = the all_gather_into_tensor (RCCL on a node) of the packed down outputs "
                     "alone, step (value) = compute and gather pipelined in `chunks` chunks (dist.choose_chunks on "
                     "the measured compute / gather times), step_1chunk = compute then gather",
             "t1_ms": round(ms(eres["t1"]), 4), "compute_ms": round(ms(eres["t_compute"]), 4),
@@ -619,8 +619,8 @@ def main():
                 xr = ep_layer_step(x, dev, world, rank, args.steps, args.warmup, coll_dev, variant=vv,
                                    median_iters=10)
                 extras[x + "_ep"] = {
-                    "what": CONFIGS[x]["name"] + f", one layer split by expert over {world} GPUs + RCCL all-gather "
-                                                 "of the layer outputs",
+                    "what": CONFIGS[x]["name"] + f", one layer split by expert over {world} GPUs + "
+                                                 f"{'RCCL' if backend == 'nccl' else backend} all-gather of the layer outputs",
                     "tflops": round(xr["total_flops"] * args.steps / xr["dt"] / 1e12, 3),
                     "step_ms": round(ms(xr["dt"]), 4), "t1_ms": round(ms(xr["t1"]), 4),
                     "compute_ms": round(ms(xr["t_compute"]), 4),
