@@ -392,6 +392,8 @@ const std::vector<Variant>& variants() {
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),
+      make_v2<kV2x | V2_TRACE | V2_TRACE_PRO>("abl_v2x_trace_pro"),
+      make_v2<kV2x | V2_TRACE | V2_TRACE_DESC>("abl_v2x_trace_desc"),
       make_v2q("x_v2q"),
       make_v2q<0, 0>("x_v2q_plain"),
       make_v2q<0, 0, 1>("x_v2q_plain_fillall"),

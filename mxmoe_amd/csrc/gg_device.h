@@ -649,6 +649,14 @@ enum : int {
   // weight-only option: the code -> fp16 constants in registers (WoK): one v_and_or_b32 per fp16
   // pair (4 / 2-bit codes), one v_perm_b32 (8-bit) — VALU-bound small-batch tiles
   WO_ANDOR = 128,
+  // with V2_TRACE (lab diagnostics, v2 staggered + B3 loop): the trace's second mark is taken after
+  // the prologue barrier (stage 0 landed) instead of after the mainloop, so the tile timeline splits
+  // off the prologue (the bit is WO_ANDOR's, which gg_v2_kernel never passes to a v2 body)
+  V2_TRACE_PRO = 128,
+  // with V2_TRACE (lab diagnostics): the second mark is taken once the tile's descriptor, problem
+  // metadata and operand pointers are in registers, right before the prologue's first LDS-DMA
+  // (the bit is WO_MSKIP's, which gg_v2_kernel never passes to a v2 body)
+  V2_TRACE_DESC = 256,
   // weight-only option (non-pipelined loop): skip the MFMAs and A reads of 16-row blocks wholly past M
   WO_MSKIP = 256,
   // with WO_SCLATE: the steady state (stage s + DIST exists) and the tail as two loops
@@ -1153,11 +1161,16 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       Half fr;
       // prologue: stage 0 (and B3: B(1)) in flight, then the first barrier
       const bool early_w = wave < HALFW;
+      if constexpr ((ABL & V2_TRACE) != 0 && (ABL & V2_TRACE_DESC) != 0) {
+        asm volatile("" ::"s"(A), "s"(B), "s"(lda), "s"(ldb), "s"(kbytes), "s"(M), "s"(N));
+        trace_mark(1);
+      }
       dma_a(0, full_stage(0), early_w);
       dma_b(0, full_stage(0), early_w);
       if (B3 && nst > 1) dma_b(1, full_stage(1), early_w);
       stage_wait(-1);
       lds_barrier();
+      if constexpr ((ABL & V2_TRACE) != 0 && (ABL & V2_TRACE_PRO) != 0) trace_mark(1);
       if constexpr (!B3) stash_scale();  // (B3: the rings fill the LDS, the stash follows the mainloop)
       uint64_t st_body = 0, st_vm = 0, st_bar = 0;
 #ifndef MXMOE_V2_NO_LATEDEAD
@@ -1416,7 +1429,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     stash_scale();
     __syncthreads();
   }
-  if constexpr ((ABL & V2_TRACE) != 0) trace_mark(1);
+  if constexpr ((ABL & V2_TRACE) != 0 && (ABL & (V2_TRACE_PRO | V2_TRACE_DESC)) == 0) trace_mark(1);
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
 
   // ---- epilogue: per-wave LDS staging of the fp16 sub-tile, 16-B row stores ----

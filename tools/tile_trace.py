@@ -54,7 +54,8 @@ def analyse(tr: np.ndarray) -> dict:
     for key in sorted(set(zip(qt.tolist(), cls.tolist()))):
         mk = (qt == key[0]) & (cls == key[1])
         per_class[f"q{key[0]}c{key[1]}"] = {"n": int(mk.sum()), "us_per_stage": round(float(np.median(dur[mk] / np.maximum(nst[mk], 1))), 3),
-                                            "median_us": round(float(np.median(dur[mk])), 2)}
+                                            "median_us": round(float(np.median(dur[mk])), 2),
+                                            "median_mark1_us": round(float(np.median((ml - st)[mk])) * TICK_US, 2)}
     xload = [round(float(dur[xcc == x].sum()) / 32, 1) for x in range(8)]
     per_cu = defaultdict(list)
     for i, k in enumerate(cu_key.tolist()):
