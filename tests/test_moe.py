@@ -102,8 +102,10 @@ def _check_batch(b, expect_rows, tags):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [256, 2048, 5632])
-def test_quant_act_bit_exact(gpu, K):
-    T, topk, E = 97, 4, 8
+# (33, 3): an odd number of routed slots, so the last wave of the two-rows-per-wave launch holds one row
+@pytest.mark.parametrize("T,topk", [(97, 4), (33, 3)])
+def test_quant_act_bit_exact(gpu, K, T, topk):
+    E = 8
     ids = _ids(T, topk, E, 1)
     h = _hidden(T, K, 2)
     tags = [0, 1, 2, 3, 1, 2, 0, 3, 1]  # shared expert last (int8)
@@ -133,8 +135,9 @@ def test_gg_permute_inp_mirror(gpu):
 # (256, 640): the shared row's quarter runs are 256, 256, 128 and 0 columns (one launch, split rows)
 @pytest.mark.parametrize("N,Ns", [(256, 512), (1408, 5632), (256, 640), (512, 512)])
 @pytest.mark.parametrize("shared_tag", [0, 1, 2, 3])
-def test_silu_mul_quant_within_one_step(gpu, N, Ns, shared_tag):
-    T, topk, E = 61, 4, 8
+@pytest.mark.parametrize("T,topk", [(61, 4), (33, 3)])
+def test_silu_mul_quant_within_one_step(gpu, N, Ns, shared_tag, T, topk):
+    E = 8
     ids = _ids(T, topk, E, 7)
     r = moe.route(ids.to(DEV), E)
     g = torch.Generator().manual_seed(8)
