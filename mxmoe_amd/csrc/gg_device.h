@@ -1157,6 +1157,10 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
       }
 #endif
     };
+    // the last stage's second 64-B half lies wholly past K (e.g. int4 at K = 1408: 704 B, 5.5 stages):
+    // its fragments are the DMA's zero fill, so neither wave group reads them or runs their MFMAs
+    // (products with zeros: the int32 sums are unchanged; f32 ones at most the sign of an exact zero)
+    const bool last_h1_empty = nst > 0 && (ks0 + nst - 1) * Cfg::BKB + Cfg::BKB / 2 >= kbytes;
     if (nst > 0) {
       Half fr;
       // prologue: stage 0 (and B3: B(1)) in flight, then the first barrier
@@ -1259,7 +1263,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           stage_wait(s);
           lds_barrier();
         }
-        hmma(fr);
+        if (!last_h1_empty) hmma(fr);  // the deferred second half of the last stage (zeros: skipped)
         if constexpr ((ABL & V2_PRIO_LATE) != 0) __builtin_amdgcn_s_setprio(0);
       } else {  // early waves
         int s = 0;
@@ -1317,8 +1321,10 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
           dma_generic(s, true);
           hread(fr, s, 0);
           hmma(fr);
-          hread(fr, s, 1);
-          hmma(fr);
+          if (!(last_h1_empty && s == nst - 1)) {
+            hread(fr, s, 1);
+            hmma(fr);
+          }
           stage_wait(s);
           lds_barrier();
         }
