@@ -378,7 +378,9 @@ const std::vector<Variant>& variants() {
       // round 5: int4 fragment reads kept unpaired (V2_I4NOPAIR: ds_read_b64 instead of 2-way-conflicted
       // ds_read2st64_b64; lab A/B mixed gate_up / down -3.1 / -1.5 %, ds2_mixed -2.1 / -1.9 %,
       // w4a4 on v2x -7.5 / -5.1 %: profiles/r05/nopair/)
-      make_v2<kV2x | WO_PIPE | WO_STAG | V2_I4NOPAIR>("v2x_256x256_w8_b3_buf_spread_edma"),
+      // + the early-wave DMA issue on int4 tiles too (V2_I4EDMA: with the unpaired reads it now pays,
+      // lab A/B w4a4 / mixed / ds2_mixed gate_up -2.7..-2.8 %, down -1.3..-3.7 %: profiles/r05/i4edma/)
+      make_v2<kV2x | WO_PIPE | WO_STAG | V2_I4NOPAIR | V2_I4EDMA>("v2x_256x256_w8_b3_buf_spread_edma"),
       // round 3 (AUTO for small-batch weight-only calls): the 64-row weight-only tile at three
       // workgroups per CU (gg_wo2_kernel<.., 3>; weight-only problems only) — profiles/r03/wo2/;
       // round 4: scale groups by LDS-DMA, register constants for the code -> fp16 step, codes
@@ -416,6 +418,7 @@ const std::vector<Variant>& variants() {
       make_v3<256, 4, 4, 3>("v3_256x256_w8_dma_ring4"),
       make_v2<kV2x>("x_v2x"),
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
+      make_v2<kV2x | V2_I4NOPAIR | V2_I4EDMA>("x_v2x_i4edma"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
       make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),

@@ -657,6 +657,10 @@ enum : int {
   // metadata and operand pointers are in registers, right before the prologue's first LDS-DMA
   // (the bit is WO_MSKIP's, which gg_v2_kernel never passes to a v2 body)
   V2_TRACE_DESC = 256,
+  // lab option: the early-wave DMA issue (V2_EARLYDMA) on int4 tiles too (round 3 measured it 2.5-4.3 %
+  // slower on w4a4, before the int4 reads were unpaired; the bit is WO_SPLIT's, which gg_v2_kernel
+  // never passes to a v2 body)
+  V2_I4EDMA = 8192,
   // weight-only option (non-pipelined loop): skip the MFMAs and A reads of 16-row blocks wholly past M
   WO_MSKIP = 256,
   // with WO_SCLATE: the steady state (stage s + DIST exists) and the tail as two loops
@@ -1067,7 +1071,7 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
     // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select)
     // (not on int4 tiles: their half stages carry twice the MFMAs, the early waves have no slack —
     //  w4a4 2.5-4.3 % slower with it, profiles/r03/lab/lab_r3.jsonl)
-    constexpr bool EDMA = (ABL & V2_EARLYDMA) != 0 && QT != QT_I4;
+    constexpr bool EDMA = (ABL & V2_EARLYDMA) != 0 && (QT != QT_I4 || (ABL & V2_I4EDMA) != 0);
     static_assert(!EDMA || (ABL & V2_BUF) != 0, "V2_EARLYDMA needs the buffer-form DMA");
     constexpr int HALFW = Cfg::WM * Cfg::WN / 2;  // SIMD partner of wave w is w + HALFW
     // one operand's pieces of stage t; `full`: no K tail in this stage (no per-lane select).
