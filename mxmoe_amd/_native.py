@@ -24,8 +24,14 @@ MXMOE_GG_ERR_UNSUPPORTED = 2
 MXMOE_GG_ERR_WORKSPACE = 3
 MXMOE_GG_ERR_HIP = 4
 
-# operand formats (MXMOE_GG_FMT_*): fp16 / integer, OCP fp8 e4m3, bfloat16
-FMT_DEFAULT, FMT_E4M3, FMT_BF16 = 0, 1, 2
+# operand formats (MXMOE_GG_FMT_*): fp16 / integer, OCP fp8 e4m3, bfloat16; FMT_F6 (w4a4 as fp6
+# images, gg_f6.h) is understood by the lab library only (measured slower)
+FMT_DEFAULT, FMT_E4M3, FMT_BF16, FMT_F6 = 0, 1, 2, 3
+
+
+def f6_row_bytes(K: int) -> int:
+    """Bytes of one fp6-image row of K int4 codes (96 per K-128 block; lab library)."""
+    return (K + 127) // 128 * 96
 
 
 class NativeLibraryError(RuntimeError):
@@ -138,6 +144,11 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_gg_plan_tiles.restype = c.c_int
     lib.mxmoe_gg_plan_tiles.argtypes = [c.POINTER(GGProblemC), c.c_int, c.c_int, c.c_void_p, c.c_void_p,
                                         c.POINTER(c.c_int)]
+    if hasattr(lib, "mxmoe_gg_pack_f6"):  # lab library only
+        lib.mxmoe_gg_pack_f6.restype = c.c_int
+        lib.mxmoe_gg_pack_f6.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int64, c.c_void_p, c.c_int64, c.c_void_p]
+        lib.mxmoe_gg_pack_f6_host.restype = c.c_int
+        lib.mxmoe_gg_pack_f6_host.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int64, c.c_void_p, c.c_int64]
     P = c.c_void_p
     lib.mxmoe_moe_route.restype = c.c_int
     lib.mxmoe_moe_route.argtypes = [P, c.c_int64, c.c_int, c.c_int, P, P, P, P, P]
@@ -257,6 +268,34 @@ def repack_weightonly(ref_words, N: int, K: int, w_bits: int):
     src = np.ascontiguousarray(ref_words, dtype=np.uint16)
     out = np.empty((N, K * w_bits // 8), dtype=np.uint8)
     check(lib().mxmoe_gg_repack_weightonly(src.ctypes.data, N, K, w_bits, out.ctypes.data))
+    return out
+
+
+def pack_f6_host(codes, K: int):
+    """Packed int4 rows (numpy uint8 [rows, K/2], pack_wxax) -> fp6 images (uint8 [rows,
+    f6_row_bytes(K)]) on the host (mxmoe_gg_pack_f6_host; lab library: MXMOE_GG_LIB)."""
+    import numpy as np
+
+    src = np.ascontiguousarray(codes, dtype=np.uint8)
+    rows = src.shape[0]
+    out = np.empty((rows, f6_row_bytes(K)), dtype=np.uint8)
+    check(lib().mxmoe_gg_pack_f6_host(src.ctypes.data, rows, K, 0, out.ctypes.data, 0))
+    return out
+
+
+def pack_f6(codes, K: int, out=None, stream=None):
+    """Packed int4 rows (uint8 device tensor [rows, K/2]) -> fp6 images on the device
+    (mxmoe_gg_pack_f6, asynchronous on ``stream`` / torch's current stream; lab library)."""
+    import torch
+
+    if codes.dtype not in (torch.uint8, torch.int8) or codes.dim() != 2 or codes.shape[1] * 2 < K:
+        raise ValueError("pack_f6: codes must be a uint8 [rows, >= K/2] tensor")
+    rows = codes.shape[0]
+    if out is None:
+        out = torch.empty((rows, f6_row_bytes(K)), dtype=torch.uint8, device=codes.device)
+    s = stream if stream is not None else torch.cuda.current_stream(codes.device)
+    check(lib().mxmoe_gg_pack_f6(ctypes.c_void_p(codes.data_ptr()), rows, K, codes.stride(0) // 2,
+                                 ctypes.c_void_p(out.data_ptr()), out.stride(0) // 2, ctypes.c_void_p(s.cuda_stream)))
     return out
 
 

@@ -26,7 +26,11 @@
 #include "../../include/mxmoe_gg.h"
 #include "gg_device.h"
 #ifdef MXMOE_LAB
+#include "gg_f6.h"   // lab-only fp6 w4a4 route: measured slower than the int4 path
 #include "gg_v2q.h"  // lab-only persistent kernel: not compiled into the product library
+// lab-only operand format: w4a4_g-1_sym with A / B as fp6 images (mxmoe_gg_pack_f6, gg_f6.h)
+#define MXMOE_GG_FMT_F6 3
+#define MXMOE_GG_F6_ROW_BYTES(K) ((((int64_t)(K) + 127) / 128) * 96)
 #endif
 
 using namespace mxmoe;
@@ -67,7 +71,7 @@ struct TileGeom {
   int bm, bn, bkb, threads;
 };
 
-enum class Kind { V0, V2, V3 };
+enum class Kind { V0, V2, V3 };  // (the fp6 kernel is planned as V3: no split-K, no XCD regions)
 
 struct Variant {
   const char* name;
@@ -253,7 +257,7 @@ Variant make_v0(const char* name) {
   v.geom[QT_F16] = {C16::BM, C16::BN, C16::BKB, C16::kThreads};
   v.geom[QT_I8] = {C8::BM, C8::BN, C8::BKB, C8::kThreads};
   v.geom[QT_I4] = {C4::BM, C4::BN, C4::BKB, C4::kThreads};
-  for (int q : {QT_W4A16, QT_W8A16, QT_I4G, QT_W2A16, QT_F8, QT_BF16}) v.geom[q] = {0, 0, 0, 0};  // v2 kernels only
+  for (int q : {QT_W4A16, QT_W8A16, QT_I4G, QT_W2A16, QT_F8, QT_BF16, QT_I4F6}) v.geom[q] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = C16::kThreads;
   v.lds_bytes = FusedCfg<C16, C8, C4>::LDS_BYTES;
   v.chunk = FusedCfg<C16, C8, C4>::LDS_BYTES <= 80 * 1024 ? 64 : 32;  // workgroups per XCD at once
@@ -270,7 +274,7 @@ Variant make_v3(const char* name) {
   v.name = name;
   v.kind = Kind::V3;
   for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {256, BN, 64, CT::NT};  // (weight-only / g128 / fp8 / bf16 cleared below)
-  for (int q : {QT_W4A16, QT_W8A16, QT_I4G, QT_W2A16, QT_F8, QT_BF16}) v.geom[q] = {0, 0, 0, 0};  // v2 kernels only
+  for (int q : {QT_W4A16, QT_W8A16, QT_I4G, QT_W2A16, QT_F8, QT_BF16, QT_I4F6}) v.geom[q] = {0, 0, 0, 0};  // v2 kernels only
   v.threads = CT::NT;
   v.lds_bytes = CT::LDS_BYTES;
   v.chunk = 32 * (160 * 1024 / CT::LDS_BYTES >= 2 ? 2 : 1);  // workgroups per XCD at once
@@ -279,6 +283,32 @@ Variant make_v3(const char* name) {
   v.launch = &launch_v3<BN, WN, NBUF, DIST, OPT>;
   return v;
 }
+
+#ifdef MXMOE_LAB
+template <int NBUF, int DIST, int OPT>
+void launch_f6(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  (void)qmask;  // QT_I4F6 only
+  hipLaunchKernelGGL((gg_f6_kernel<NBUF, DIST, OPT>), dim3(grid), dim3(512), 0, s, a);
+}
+
+// fp6 w4a4 tiles (gg_f6.h): 256 x 256 (+ 128-row tail class), one 512-thread workgroup per CU
+template <int NBUF, int DIST, int OPT = 0>
+Variant make_f6(const char* name) {
+  typedef F6Cfg<256, 256, 2, 4, NBUF, DIST> CT;
+  Variant v;
+  v.name = name;
+  v.kind = Kind::V3;
+  for (int q = 0; q < QT_COUNT; ++q) v.geom[q] = {0, 0, 0, 0};
+  v.geom[QT_I4F6] = {256, 256, CT::SKB, CT::NT};
+  v.threads = CT::NT;
+  v.lds_bytes = CT::LDS_BYTES;
+  v.chunk = 32;
+  v.k_stage_bytes = 0;  // (image rows are whole stages by construction)
+  v.tail_bm = 128;
+  v.launch = &launch_f6<NBUF, DIST, OPT>;
+  return v;
+}
+#endif  // MXMOE_LAB
 
 // the v2 family's geometry (launch set by the caller)
 Variant v2_base(const char* name, int lds_bytes) {
@@ -290,6 +320,7 @@ Variant v2_base(const char* name, int lds_bytes) {
   v.geom[QT_W8A16] = {256, 256, 64, 512};
   v.geom[QT_W2A16] = {256, 256, 16, 512};  // 64-K stages: 16 B of 2-bit codes per row
   v.geom[QT_I4G] = {256, 256, 128, 512};  // w4a4 g128 (gg_tile_g128): 256 / 128-row classes as int4
+  v.geom[QT_I4F6] = {0, 0, 0, 0};         // fp6 images: the f6 kernel only
   v.threads = 512;
   v.lds_bytes = lds_bytes;
   v.chunk = 32;  // one 512-thread workgroup per CU, 32 CUs per XCD
@@ -438,6 +469,12 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_edma2_stamp"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_STAMP | (4 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_sp4_stamp"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
+      // round 5: w4a4 on fp6 images and the fp6 MFMA (gg_f6.h; exact, 9-18 % slower than v3's int4
+      // tiles on the layer calls: profiles/r05/f6/); OPT 1 unpaired reads, 2 spread DMA
+      make_f6<3, 2>("f6_256x256_w8_ring3"),
+      make_f6<3, 2, 1>("xf6_nopair"),
+      make_f6<3, 2, 2>("xf6_spread"),
+      make_f6<3, 2, 3>("xf6_nopair_spread"),
       // timing ablations of the staggered v2 (WRONG RESULTS by design; int8 tiles only)
       make_v2<V2_STAGGER | ABL_NO_DMA>("abl_v2s_nodma"),
       make_v2<V2_STAGGER | ABL_NO_EPI>("abl_v2s_noepi"),
@@ -468,6 +505,9 @@ const std::vector<Variant>& variants() {
 constexpr const char* kDefaultVariantName = "v2x_256x256_w8_b3_buf_spread_edma";
 constexpr const char* kInt4Variant = "v3_256x128_w4_dma_ring3_2wg";
 constexpr const char* kWoSmallVariant = "wo3_64x256_w8_3wg";
+#ifdef MXMOE_LAB
+constexpr const char* kF6Variant = "f6_256x256_w8_ring3";
+#endif
 // weight-only calls whose rows per weight byte are this small or smaller run kWoSmallVariant:
 // the weight-bytes-weighted mean M over the call's problems (qwen2_moe layer 11: ~60 at bs = 128,
 // ~250 at bs = 2048, ~1030 at bs = 8192, where v2x's 256-row tiles are as fast or faster)
@@ -506,6 +546,16 @@ int qtype_of(int a_bits, int w_bits, int gsize, int sym, int fmt, int* qt) {
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported: w%da%d bf16 (only 16-bit bf16 operands)", w_bits,
                 a_bits);
   }
+#ifdef MXMOE_LAB
+  if (fmt == MXMOE_GG_FMT_F6) {  // w4a4_g-1_sym with fp6 images of the int4 codes (mxmoe_gg_pack_f6)
+    if (a_bits == 4 && w_bits == 4 && gsize == -1 && sym) {
+      *qt = QT_I4F6;
+      return MXMOE_GG_OK;
+    }
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "quant type not supported: w%da%d_g%d_%s as fp6 images (only w4a4_g-1_sym)",
+                w_bits, a_bits, gsize, sym ? "sym" : "asym");
+  }
+#endif
   if (fmt != MXMOE_GG_FMT_DEFAULT) return fail(MXMOE_GG_ERR_UNSUPPORTED, "unknown operand format %d", fmt);
   if (a_bits == 16 && w_bits == 16) {
     *qt = QT_F16;
@@ -610,7 +660,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
                 idx, v.name, p.w_bits, p.a_bits);
   if (is_weightonly(qt)) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
   const int abits = is_float16(qt) ? 16 : p.a_bits;
-  const int64_t kbits = (int64_t)p.K * abits;
+  const int64_t kbits = (int64_t)p.K * abits;  // (fp6 images: K of the int4 codes they encode)
   if (kbits % 128 != 0)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d must be a multiple of %d for %d-bit data (16-B rows)", idx,
                 p.K, (int)(128 / abits), abits);
@@ -622,7 +672,12 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (qt != QT_F16 && qt != QT_BF16 && qt != QT_F8 && p.K > 131072)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: K=%d exceeds the exact int32 accumulation bound 131072", idx, p.K);
   if (p.N % 8 != 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: N=%d must be a multiple of 8", idx, p.N);
+  // fp6 images: 96 B per K-128 block, K padded to whole blocks (mxmoe_gg_pack_f6)
+#ifdef MXMOE_LAB
+  const int64_t kbytes = qt == QT_I4F6 ? (int64_t)MXMOE_GG_F6_ROW_BYTES(p.K) : kbits / 8;
+#else
   const int64_t kbytes = kbits / 8;
+#endif
   const int64_t lda_b = p.lda ? p.lda * 2 : kbytes;
   const int64_t ldb_b = p.ldb ? p.ldb * 2 : kbytes;
   const int64_t ldc = p.ldc ? p.ldc : p.N;
@@ -693,8 +748,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   };
   auto full_tile_cost = [&](int i) {
     const GGMeta& m = all[i];
-    // int4: 2 MFMA passes per staged byte; g128 adds the per-group f32 fold (~25 %)
-    const double passes = m.qtype == QT_I4 ? 2.0 : m.qtype == QT_I4G ? 2.5 : 1.0;
+    // int4: 2 MFMA passes per staged byte; g128 adds the per-group f32 fold (~25 %); fp6 images:
+    // one fp6 MFMA (the int8 one's cycles) per 96 B of K-128
+    const double passes = m.qtype == QT_I4 ? 2.0 : m.qtype == QT_I4G ? 2.5 : m.qtype == QT_I4F6 ? 128.0 / 96 / 2 : 1.0;
     return passes * (double)m.kbytes * v.geom[m.qtype].bm * v.geom[m.qtype].bn;
   };
   // m-tiles of a problem: (m0, class); v2 classes 256 / 128 / 64 rows (see Variant::tail_bm)
@@ -762,8 +818,9 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       bytes = rows * 128 + cols * 64 * (m.qtype == QT_W2A16 ? 2 : m.qtype == QT_W4A16 ? 4 : 8) / 8.0;
       equiv = 2.0 * rows * cols * 64 / 128;
     } else {
-      const double kel = g.bkb * 8.0 / (is_float16(m.qtype) ? 16 : (m.qtype == QT_I8 || m.qtype == QT_F8) ? 8 : 4);
-      const double rate = is_float16(m.qtype) ? 128 : 256, fold = m.qtype == QT_I4G ? 1.25 : 1.0;
+      const double kel = m.qtype == QT_I4F6 ? 128.0
+                       : g.bkb * 8.0 / (is_float16(m.qtype) ? 16 : (m.qtype == QT_I8 || m.qtype == QT_F8) ? 8 : 4);
+      const double rate = is_float16(m.qtype) ? 128 : m.qtype == QT_I4F6 ? 512 : 256, fold = m.qtype == QT_I4G ? 1.25 : 1.0;
       bytes = (rows + cols) * g.bkb;
       equiv = 2.0 * rows * cols * kel / rate * fold;
     }
@@ -1178,6 +1235,16 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
       }
     }
   }
+#ifdef MXMOE_LAB
+  if ((mask & (1 << QT_I4F6)) && mask != (1 << QT_I4F6))
+    return fail(MXMOE_GG_ERR_UNSUPPORTED,
+                "fp6-image w4a4 problems (MXMOE_GG_FMT_F6) cannot share a call with other quant types: plan them "
+                "as a call of their own");
+  if (mask == (1 << QT_I4F6)) {  // fp6 images: the fp6 kernel (no other variant reads them)
+    *out = variant_index(kF6Variant);
+    return MXMOE_GG_OK;
+  }
+#endif
   if (mask == (1 << QT_I4)) {
     // int4-only: the 256x128 2-WG/CU kernel, unless the call is low-fill enough for the v2s plan
     // to split K (that kernel cannot)
@@ -1265,9 +1332,9 @@ int mxmoe_gg_default_variant(void) { return variant_index(kDefaultVariantName); 
 
 int mxmoe_gg_list_variants(char* buf, size_t n) {
   // weight-only kernels cover every group size / sym of a bit width: listed under the base name
-  static const char* qnames[QT_COUNT] = {"fp16",          "w8a8_g-1_sym", "w4a4_g-1_sym", "w4a16",           "w8a16",
-                                         "w4a4_g128_sym", "w2a16",        "w8a8_g-1_sym_E4M3", "bf16"};
-  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4, 2, 8, 16};
+  static const char* qnames[QT_COUNT] = {"fp16",          "w8a8_g-1_sym", "w4a4_g-1_sym",      "w4a16", "w8a16",
+                                         "w4a4_g128_sym", "w2a16",        "w8a8_g-1_sym_E4M3", "bf16",  "w4a4_g-1_sym_F6"};
+  static const int wbits[QT_COUNT] = {16, 8, 4, 4, 8, 4, 2, 8, 16, 6};
   std::string out;
   const auto& vs = variants();
   for (size_t i = 0; i < vs.size(); ++i) {
@@ -1308,6 +1375,55 @@ int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int3
   if (threads) *threads = g.threads;
   return MXMOE_GG_OK;
 }
+
+#ifdef MXMOE_LAB
+// lab-only exports (tools/f6_bench.py, tests/test_f6.py): int4 rows -> fp6 images (gg_f6.h layout)
+namespace {
+int f6_args(const void* src, int rows, int K, int64_t ld_src, const void* dst, int64_t ld_dst, int64_t* ls, int64_t* ld) {
+  if (rows < 0 || K < 0 || (rows > 0 && (!src || !dst))) return fail(MXMOE_GG_ERR_INVALID, "pack_f6: bad arguments");
+  if (K % 32) return fail(MXMOE_GG_ERR_INVALID, "pack_f6: K=%d must be a multiple of 32 (16-B int4 rows)", K);
+  *ls = ld_src ? ld_src * 2 : K / 2;
+  *ld = ld_dst ? ld_dst * 2 : MXMOE_GG_F6_ROW_BYTES(K);
+  if (*ls < K / 2 || *ld < MXMOE_GG_F6_ROW_BYTES(K) || (*ls % 16) || (*ld % 16))
+    return fail(MXMOE_GG_ERR_INVALID, "pack_f6: row strides must cover the row and be multiples of 8 words");
+  if (rows > 0 && (((uintptr_t)src | (uintptr_t)dst) & 15))
+    return fail(MXMOE_GG_ERR_INVALID, "pack_f6: buffers must be 16-B aligned");
+  return MXMOE_GG_OK;
+}
+}  // namespace
+
+int mxmoe_gg_pack_f6(const void* src, int rows, int K, int64_t ld_src, void* dst, int64_t ld_dst, void* stream) {
+  int64_t ls, ld;
+  int st = f6_args(src, rows, K, ld_src, dst, ld_dst, &ls, &ld);
+  if (st) return st;
+  const int64_t threads = (int64_t)rows * ((K + 127) / 128) * 4;
+  if (threads == 0) return MXMOE_GG_OK;
+  hipLaunchKernelGGL(f6_pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const uint8_t*>(src), ls, static_cast<uint8_t*>(dst), ld, rows, K);
+  HIP_TRY(hipGetLastError());
+  return MXMOE_GG_OK;
+}
+
+int mxmoe_gg_pack_f6_host(const void* src, int rows, int K, int64_t ld_src, void* dst, int64_t ld_dst) {
+  int64_t ls, ld;
+  int st = f6_args(src, rows, K, ld_src, dst, ld_dst, &ls, &ld);
+  if (st) return st;
+  const int nblk = (K + 127) / 128;
+  for (int64_t r = 0; r < rows; ++r)
+    for (int b = 0; b < nblk; ++b)
+      for (int g = 0; g < 4; ++g) {
+        const int e0 = b * 128 + g * 32;
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (e0 < K) memcpy(w, static_cast<const uint8_t*>(src) + r * ls + e0 / 2, 16);  // (K % 32 == 0)
+        uint32_t d[6];
+        f6_pack32(w, d);
+        uint8_t* o = static_cast<uint8_t*>(dst) + r * ld + b * 96;
+        memcpy(o + g * 16, d, 16);
+        memcpy(o + 64 + g * 8, d + 4, 8);
+      }
+  return MXMOE_GG_OK;
+}
+#endif  // MXMOE_LAB
 
 int mxmoe_gg_resolve_variant(const mxmoe_gg_problem* problems, int problem_count, int variant, int* out) {
   if (!out) return fail(MXMOE_GG_ERR_INVALID, "out is NULL");

@@ -34,12 +34,15 @@ namespace mxmoe {
 // QT_I4G: w4a4_g128_sym (A and B int4 with one fp16 scale per 128-K group)
 // QT_F8: w8a8_g-1_sym_E4M3 (A and B OCP fp8 e4m3, per-channel fp16 scales, f32 accumulate)
 // QT_BF16: bf16 A and B, f32 accumulate, fp16 C
+// QT_I4F6: w4a4_g-1_sym with A and B given as fp6 e3m2 images of the int4 codes (gg_f6.h): the
+//          block-scaled fp6 MFMA, f32 accumulate (exact: integer partial sums below 2^24)
 enum QType : int32_t {
   QT_F16 = 0, QT_I8 = 1, QT_I4 = 2, QT_W4A16 = 3, QT_W8A16 = 4, QT_I4G = 5, QT_W2A16 = 6, QT_F8 = 7, QT_BF16 = 8,
-  QT_COUNT = 9
+  QT_I4F6 = 9,
+  QT_COUNT = 10
 };
 // quant types whose epilogue applies the per-channel scales sa[m] * sb[n]
-constexpr bool qt_scaled(int qt) { return qt == QT_I8 || qt == QT_I4 || qt == QT_F8; }
+constexpr bool qt_scaled(int qt) { return qt == QT_I8 || qt == QT_I4 || qt == QT_F8 || qt == QT_I4F6; }
 
 // One row of the plan table (64 B), written by the host planner into the workspace.
 struct GGMeta {
@@ -156,6 +159,10 @@ struct AccT<QT_F8> {
 };
 template <>
 struct AccT<QT_BF16> {
+  typedef v4f type;
+};
+template <>
+struct AccT<QT_I4F6> {
   typedef v4f type;
 };
 
@@ -1804,6 +1811,7 @@ __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>:
     for (int j = 0; j < FN; ++j) {
       uint2 pk;
       if constexpr (QT == QT_F16) pk = pack4_f16(acc[i][j]);
+      else if constexpr (QT == QT_I4F6) pk = scale_pack4f(acc[i][j], sai, sbw[j]);  // f32 acc = the int32 sum
       else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
       const int q = 2 * j + (g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * RB + ((q ^ (ml & (CPR - 1))) << 4) + (g & 1) * 8) = pk;

@@ -24,15 +24,17 @@ import torch
 from . import _native as nat
 
 
-FMT_CODES = {"": nat.FMT_DEFAULT, "E4M3": nat.FMT_E4M3, "bf16": nat.FMT_BF16}
+FMT_CODES = {"": nat.FMT_DEFAULT, "E4M3": nat.FMT_E4M3, "bf16": nat.FMT_BF16, "F6": nat.FMT_F6}
 
 
 @dataclasses.dataclass(frozen=True)
 class QParams:
     """Per-problem quantisation parameters (reference QParams, quantize.cuh:14-25).
 
-    ``fmt``: "" (fp16 / two's-complement integers), "E4M3" (w8a8_g-1_sym_E4M3: OCP fp8 codes) or
-    "bf16" (16-bit bfloat16 operands). The reference's ``_accfp16`` strategies (fp16 MMA with an fp16
+    ``fmt``: "" (fp16 / two's-complement integers), "E4M3" (w8a8_g-1_sym_E4M3: OCP fp8 codes),
+    "bf16" (16-bit bfloat16 operands) or "F6" (w4a4_g-1_sym with A and B as fp6 images of the int4
+    codes, ``_native.pack_f6``: same results on the fp6 MFMA — lab library only, measured slower
+    than the int4 path). The reference's ``_accfp16`` strategies (fp16 MMA with an fp16
     accumulator, tile_config.py:94-97) run as their f32-accumulating base type: MFMA has no fp16
     accumulator, and the f32 sum is the more accurate result of the same products."""
 
@@ -68,7 +70,7 @@ class QParams:
         if not self.is_quant:
             return "bf16" if self.fmt == "bf16" else "fp16"
         return f"w{self.w_bits}a{self.a_bits}_g{self.gsize}_{'sym' if self.sym else 'asym'}" + \
-            ("_E4M3" if self.is_fp8 else "")
+            ("_E4M3" if self.is_fp8 else "_F6" if self.fmt == "F6" else "")
 
     @staticmethod
     def from_qcfg(qcfg: str) -> "QParams":
@@ -82,7 +84,8 @@ class QParams:
         g = int(qcfg.split("_g")[1].split("_")[0])
         if qcfg.endswith("_bf16"):
             raise ValueError(f"{qcfg}: weight-only with bf16 activations is not built on MI355X")
-        return QParams(a_bits=a, w_bits=w, gsize=g, sym="asym" not in qcfg, fmt="E4M3" if qcfg.endswith("_E4M3") else "")
+        fmt = "E4M3" if qcfg.endswith("_E4M3") else "F6" if qcfg.endswith("_F6") else ""
+        return QParams(a_bits=a, w_bits=w, gsize=g, sym="asym" not in qcfg, fmt=fmt)
 
 
 FP16 = QParams()
@@ -90,6 +93,7 @@ BF16 = QParams(fmt="bf16")
 W8A8 = QParams(8, 8, -1, True)
 W8A8_E4M3 = QParams(8, 8, -1, True, "E4M3")  # w8a8_g-1_sym_E4M3: OCP fp8 operands, f32 accumulate
 W4A4 = QParams(4, 4, -1, True)
+W4A4_F6 = QParams(4, 4, -1, True, "F6")  # w4a4_g-1_sym on fp6 images (lab library: nat.pack_f6 of A and B)
 W4A4_G128 = QParams(4, 4, 128, True)  # w4a4_g128_sym: one scale per 128-K group (cta_gemm.cuh:610-772)
 # weight-only (any group size that is -1 or a multiple of 64 dividing K, sym or asym, 2 / 4 / 8 bits)
 W4A16_G128_ASYM = QParams(16, 4, 128, False)

@@ -85,6 +85,54 @@ def build_layer_inputs(shapes: Sequence[QShape], device="cuda", seed: int = 42,
     return LayerInputs(problems=probs, shapes=list(shapes))
 
 
+class F6Layer:
+    """A w4a4 call run on fp6 images (MXMOE_GG_FMT_F6, gg_f6.h): the B images are made once (weight
+    preparation, as a serving stack keeps prepared weights), the A rows of every problem sit in one
+    packed int4 buffer per K (as the MoE quantiser writes one permuted activation buffer) and
+    ``pack_a()`` rebuilds their images — one mxmoe_gg_pack_f6 launch per distinct K, on the current
+    stream — before each GEMM. ``problems`` read the images; results equal the int4 call's bit for bit."""
+
+    def __init__(self, inputs: "LayerInputs"):
+        from . import _native as nat
+        from .groupgemm import W4A4_F6
+
+        self.shapes = inputs.shapes
+        ps = inputs.problems
+        if any(p.q.qcfg != "w4a4_g-1_sym" for p in ps):
+            raise ValueError("F6Layer: every problem must be w4a4_g-1_sym")
+        dev = ps[0].C.device if ps else torch.device("cuda")
+        self.a_groups = []  # (int4 rows [R, K/2], K, images [R, f6_row_bytes(K)])
+        row_of = {}
+        for K in sorted({p.K for p in ps}):
+            sel = [i for i, p in enumerate(ps) if p.K == K]
+            a4 = torch.cat([ps[i].A.reshape(max(ps[i].M, 0), K // 2) for i in sel]) if sel else None
+            img = torch.empty((a4.shape[0], nat.f6_row_bytes(K)), dtype=torch.uint8, device=dev)
+            r = 0
+            for i in sel:
+                row_of[i] = (len(self.a_groups), r)
+                r += ps[i].M
+            self.a_groups.append((a4, K, img))
+        self.problems = []
+        for i, p in enumerate(ps):
+            g, r = row_of[i]
+            img = self.a_groups[g][2]
+            self.problems.append(dataclasses.replace(p, q=W4A4_F6, A=img[r:r + p.M], B=nat.pack_f6(p.B.reshape(p.N, p.K // 2), p.K),
+                                                     lda=0, ldb=0))
+        self.pack_a()
+        torch.cuda.current_stream(dev).synchronize()
+
+    def pack_a(self) -> None:
+        from . import _native as nat
+
+        for a4, K, img in self.a_groups:
+            if a4.shape[0]:
+                nat.pack_f6(a4, K, out=img)
+
+    @property
+    def flops(self) -> int:
+        return sum(s.flops for s in self.shapes)
+
+
 def refill_layer_inputs(inp: LayerInputs, seed: int = 42) -> None:
     """Regenerate a call's operands (the same seeded values as build_layer_inputs) in place, so a
     plan made on the buffers stays valid: operands materialised after planning, as a serving loop

@@ -275,3 +275,13 @@ def test_splitk_planning():
     layer = load_workload(qwen2_layer11_workload(8192))["layer-11"]["down"]
     probs = [_prob(M=s.M, N=s.N, K=s.K, a_bits=16, w_bits=16, scale_a=0, scale_b=0) for s in layer]
     assert ws(probs, v2s) < 1 << 20  # table only
+
+
+def test_product_library_rejects_fp6_images():
+    """MXMOE_GG_FMT_F6 (w4a4 as fp6 images) is a lab-library route: the
+    product library refuses the format instead of running it."""
+    p = nat.GGProblemC(A=16, B=16, scale_a=16, scale_b=16, C=16, M=64, N=256, K=256, a_bits=4, w_bits=4, gsize=-1,
+                       sym=1, fmt=nat.FMT_F6, lda=0, ldb=0, ldc=0)
+    arr = (nat.GGProblemC * 1)(p)
+    with pytest.raises(nat.GGError, match="unknown operand format"):
+        nat.workspace_size(arr, 1, nat.VARIANT_AUTO)
