@@ -203,9 +203,12 @@ __device__ __forceinline__ float amax8(const h8_t& x) {
 }
 
 // One WAVE per slot row (4 rows per 256-thread workgroup): lane l holds elements c*512 + 8l .. +7
-// of chunk c in registers (MAXC chunks: rows up to MAXC*512 elements), so every lane has MAXC
-// independent 16-B loads in flight, the per-token amax is a wave butterfly and a 128-element group
-// is 16 adjacent lanes — no LDS, no barrier. parts == 4: the workgroups from blk_shared on take one
+// of chunk c in registers (MAXC chunks: rows up to MAXC*512 elements, MAXC = the launch's widest
+// row in 512-element chunks), so every lane has MAXC independent 16-B loads in flight, the
+// per-token amax is a wave butterfly and a 128-element group is 16 adjacent lanes — no LDS, no
+// barrier. Loads and the SiLU are straight-line over all MAXC chunks (lanes past the row read the
+// row's first 16 B and zero them by a select): per-chunk branches kept the scheduler from
+// interleaving the chunks' dependency chains (v_exp / v_rcp latency, packed-math wait states). parts == 4: the workgroups from blk_shared on take one
 // wide shared row each, wave w its w-th run of 128-aligned columns (the per-token amax then crosses
 // the 4 waves through LDS), so routed and shared rows share one launch and one register budget.
 template <bool SILU, int MAXC>
@@ -236,7 +239,8 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const int qw = split_row ? ((sg.width / 4 + 127) & ~127) : sg.width;
   const int col0 = part * qw;
   const int width = split_row ? max(0, min(qw, sg.width - col0)) : sg.width;
-  row_src += col0;
+  // (a wave whose quarter of a split row is empty keeps a valid address: the row's start)
+  const _Float16* const base = width > 0 ? row_src + col0 : row_src;
 
   // every load of the row first (all in flight together), then the arithmetic
   h8_t x[MAXC];
@@ -244,17 +248,19 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int idx = c * 512 + lane * 8;
-    x[c] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    if constexpr (SILU) u[c] = h8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    if (idx < width) {
-      x[c] = *reinterpret_cast<const h8_t*>(row_src + idx);
-      if constexpr (SILU) u[c] = *reinterpret_cast<const h8_t*>(row_src + upoff + idx);
+    const bool in = idx < width;
+    const int li = in ? idx : 0;
+    const uint4 xv = *reinterpret_cast<const uint4*>(base + li);
+    const uint4 z = {0, 0, 0, 0};
+    x[c] = __builtin_bit_cast(h8_t, in ? xv : z);
+    if constexpr (SILU) {
+      const uint4 uv = *reinterpret_cast<const uint4*>(base + upoff + li);
+      u[c] = __builtin_bit_cast(h8_t, in ? uv : z);
     }
   }
   if constexpr (SILU) {
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c * 512 < width)  // uniform: chunks past the row stay zero (silu(0) * 0 = 0)
+    for (int c = 0; c < MAXC; ++c) {  // (zeros past the row: silu(0) * 0 = 0)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         // silu(g) = g / (1 + e^-g) with the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: the
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   }
 
   if (sg.qtag == MXMOE_ACT_FP16) {
-    _Float16* o = reinterpret_cast<_Float16*>(a.out + sg.out_off) + row * sg.width + col0;
+    _Float16* o = reinterpret_cast<_Float16*>(a.out + sg.out_off) + row * sg.width + col0;  // (width 0: no store)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int idx = c * 512 + lane * 8;
@@ -309,12 +315,22 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const _Float16 sc = rtn_scale(m, qmax);
   const float rs = __builtin_amdgcn_rcpf((float)sc);
   if (lane == 0 && part == 0) a.scales[sg.scale_off + row] = sc;
+  // every chunk's codes first (straight-line: the chunks' packed-math chains interleave), then the
+  // predicated stores
+  if (bits == 8) {
+    uint2 q[MAXC];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    const int idx = c * 512 + lane * 8;
-    if (idx >= width) continue;
-    if (bits == 8) *reinterpret_cast<uint2*>(o + idx) = codes_i8(x[c], (float)sc, rs, lim);
-    else *reinterpret_cast<uint32_t*>(o + idx / 2) = codes_i4(x[c], (float)sc, rs, lim);
+    for (int c = 0; c < MAXC; ++c) q[c] = codes_i8(x[c], (float)sc, rs, lim);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c * 512 + lane * 8 < width) *reinterpret_cast<uint2*>(o + c * 512 + lane * 8) = q[c];
+  } else {
+    uint32_t q[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) q[c] = codes_i4(x[c], (float)sc, rs, lim);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c * 512 + lane * 8 < width) *reinterpret_cast<uint32_t*>(o + (c * 512 + lane * 8) / 2) = q[c];
   }
 }
 
@@ -354,14 +370,21 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 using namespace mxmoe;
 
+// registers sized to the widest row of the launch, in 512-element chunks (1408 -> 3, 2048 -> 4)
 template <bool SILU>
 static void launch_act_w(const ActArgs& a, int maxw, hipStream_t st) {
   const int64_t blocks = a.parts > 1 ? a.blk_shared + (a.nslots - a.ntk)
                                      : (a.nslots - a.s0 + kThreads / 64 - 1) / (kThreads / 64);
   const dim3 grid((unsigned)blocks), block(kThreads);
-  if (maxw <= 2048) hipLaunchKernelGGL((act_quant_kernel<SILU, 4>), grid, block, 0, st, a);
-  else if (maxw <= 4096) hipLaunchKernelGGL((act_quant_kernel<SILU, 8>), grid, block, 0, st, a);
-  else if (maxw <= 8192) hipLaunchKernelGGL((act_quant_kernel<SILU, 16>), grid, block, 0, st, a);
+  const int nc = (maxw + 511) / 512;
+  if (nc <= 1) hipLaunchKernelGGL((act_quant_kernel<SILU, 1>), grid, block, 0, st, a);
+  else if (nc <= 2) hipLaunchKernelGGL((act_quant_kernel<SILU, 2>), grid, block, 0, st, a);
+  else if (nc <= 3) hipLaunchKernelGGL((act_quant_kernel<SILU, 3>), grid, block, 0, st, a);
+  else if (nc <= 4) hipLaunchKernelGGL((act_quant_kernel<SILU, 4>), grid, block, 0, st, a);
+  else if (nc <= 6) hipLaunchKernelGGL((act_quant_kernel<SILU, 6>), grid, block, 0, st, a);
+  else if (nc <= 8) hipLaunchKernelGGL((act_quant_kernel<SILU, 8>), grid, block, 0, st, a);
+  else if (nc <= 12) hipLaunchKernelGGL((act_quant_kernel<SILU, 12>), grid, block, 0, st, a);
+  else if (nc <= 16) hipLaunchKernelGGL((act_quant_kernel<SILU, 16>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((act_quant_kernel<SILU, 32>), grid, block, 0, st, a);
 }
 
