@@ -469,6 +469,9 @@ const std::vector<Variant>& variants() {
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_EARLYDMA | V2_STAMP | (2 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_edma2_stamp"),
       make_v2<V2_STAGGER | V2_B3 | V2_BUF | V2_STAMP | (4 << V2_SPREAD_SHIFT)>("abl_v2s3_buf_sp4_stamp"),
       make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),
+      // round 5: v3 at one wave per SIMD on 256 x 256 tiles (128 x 128 wave tiles, accumulators in
+      // AGPRs: half the int4 widening per MFMA) — 23-33 % slower, profiles/r05/v3w/
+      make_v3<256, 2, 4, 3, 4>("x_v3_256x256_w4_1wg"),
       // round 5: w4a4 on fp6 images and the fp6 MFMA (gg_f6.h; exact, 9-18 % slower than v3's int4
       // tiles on the layer calls: profiles/r05/f6/); OPT 1 unpaired reads, 2 spread DMA
       make_f6<3, 2>("f6_256x256_w8_ring3"),

@@ -2030,8 +2030,10 @@ __device__ __forceinline__ void gg_tile_v3(const GGMeta& mt, const uint8_t* __re
 
 // QM = set of quant types compiled in (bit 1 << QType, chosen by the plan): a single-type launch
 // carries one tile body, not three
+// OPT & 4: one workgroup per CU, one wave per SIMD (512 registers: the accumulators of a 128 x 128
+// wave tile live in AGPRs) — the 4-wave 256 x 256 tile widens each int4 fragment for 8 MFMAs, not 4
 template <int BN, int WN, int NBUF, int DIST, int QM, int OPT = 0>
-__global__ __launch_bounds__(128 * WN, 2) void gg_v3_kernel(GGArgs args) {  // 2 waves/SIMD: <= 256 VGPRs
+__global__ __launch_bounds__(128 * WN, (OPT & 4) ? 1 : 2) void gg_v3_kernel(GGArgs args) {  // 2 waves/SIMD: <= 256 VGPRs
   typedef V3Cfg<256, BN, WN, NBUF, DIST> CT;
   typedef V3Cfg<128, BN, WN, NBUF, DIST> CS;
   __shared__ __attribute__((aligned(16))) uint8_t lds[CT::LDS_BYTES];
