@@ -61,6 +61,16 @@ enum {
   MXMOE_GG_FMT_BF16 = 2     /* bf16: 16-bit operands are bfloat16                              */
 };
 
+/* Epilogue flag, OR-ed into mxmoe_gg_problem.fmt (fp16, w8a8_g-1_sym and w4a4_g-1_sym problems, v2x
+ * and v3 variants; no reference counterpart — it fuses the MoE layer's silu_mul_then_quant
+ * activation, ref_bind.cu:595-757, into the gate_up GroupGEMM). B holds N = 2 Nh rows interleaved
+ * in 16-row blocks: rows [32 b, 32 b + 16) are gate rows [16 b, 16 b + 16) and rows
+ * [32 b + 16, 32 b + 32) the matching up rows (scale_b permuted alike; N % 32 == 0). C is [M][Nh]
+ * (ldc >= Nh, 0 = Nh): C[m][n] = fp16_rn(silu(f32 g) * f32 u) with g, u the fp16 outputs the call
+ * would have written for gate column n and up column n, silu(g) = g * rcp(1 + exp2(-g log2 e)) —
+ * the arithmetic of mxmoe_moe_silu_mul_quant, bit for bit. */
+#define MXMOE_GG_EPI_SILU_MUL 0x100
+
 /* Same memory layout as the reference's mxmoe::QParams (quantize.cuh:14-25):
  * int2 qbits {x = a_bits, y = w_bits}; int gsize; bool sym; padded to 16 bytes, 8-byte aligned.
  * The three bytes after `sym` are the reference's padding: its QParams constructors

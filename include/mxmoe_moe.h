@@ -76,6 +76,14 @@ int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64
                              const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg, void* out,
                              void* scales, void* stream);
 
+/* mxmoe_moe_silu_mul_quant's quantisation alone, for activations the gate_up GroupGEMM already
+ * produced with its fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL, include/mxmoe_gg.h): routed_in fp16
+ * [T*topk][N] in slot order, shared_in fp16 [T][N_shared] or NULL; same segments, outputs and limits.
+ * (No reference counterpart: the reference's silu_mul_then_quant, ref_bind.cu:595-757, does both.) */
+int mxmoe_moe_quant_slots(const void* routed_in, const void* shared_in, int64_t T, int topk, int N, int N_shared,
+                          const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg, void* out, void* scales,
+                          void* stream);
+
 /* out[t][h] = fp16_rn(acc), acc = +0 then, for k = 0..topk-1 in order,
  *   acc = fma(weights[t][k], f32(y[inv_slot[t*topk + k]][h]), acc),
  * then, if shared != NULL, acc = fma(shared_w ? shared_w[t] : 1, f32(shared[t][h]), acc).

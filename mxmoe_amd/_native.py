@@ -27,6 +27,7 @@ MXMOE_GG_ERR_HIP = 4
 # operand formats (MXMOE_GG_FMT_*): fp16 / integer, OCP fp8 e4m3, bfloat16; FMT_F6 (w4a4 as fp6
 # images, gg_f6.h) is understood by the lab library only (measured slower)
 FMT_DEFAULT, FMT_E4M3, FMT_BF16, FMT_F6 = 0, 1, 2, 3
+EPI_SILU_MUL = 0x100  # MXMOE_GG_EPI_SILU_MUL: fmt flag, C = silu(gate) * up (include/mxmoe_gg.h)
 
 
 def f6_row_bytes(K: int) -> int:
@@ -88,7 +89,7 @@ EXPORTED_SYMBOLS = (
     "groupgemm_mxmoe", "groupgemm_mxmoe_fmt", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     "mxmoe_gg_plan_tiles",
     # include/mxmoe_moe.h (MoE-layer plumbing)
-    "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_combine",
+    "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_quant_slots", "mxmoe_moe_combine",
 )
 
 
@@ -156,6 +157,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_moe_quant_act.argtypes = [P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, P, c.c_int, P, P, P]
     lib.mxmoe_moe_silu_mul_quant.restype = c.c_int
     lib.mxmoe_moe_silu_mul_quant.argtypes = [P, P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, c.c_int, P, P, P]
+    if hasattr(lib, "mxmoe_moe_quant_slots"):  # (builds before round 5's fused SiLU epilogue lack it: A/B tools)
+        lib.mxmoe_moe_quant_slots.restype = c.c_int
+        lib.mxmoe_moe_quant_slots.argtypes = [P, P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, c.c_int, P, P, P]
     lib.mxmoe_moe_combine.restype = c.c_int
     lib.mxmoe_moe_combine.argtypes = [P, P, P, P, P, c.c_int64, c.c_int, c.c_int, P, P]
 

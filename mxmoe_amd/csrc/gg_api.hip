@@ -533,6 +533,7 @@ int variant_index(const char* name) {
 }
 
 int qtype_of(int a_bits, int w_bits, int gsize, int sym, int fmt, int* qt) {
+  fmt &= 0xFF;  // (epilogue flags, MXMOE_GG_EPI_*, live above the operand format)
   if (fmt == MXMOE_GG_FMT_E4M3) {  // w8a8_g-1_sym_E4M3 (tile_config.py:45, 104-106, 192)
     if (a_bits == 8 && w_bits == 8 && gsize == -1 && sym) {
       *qt = QT_F8;
@@ -661,6 +662,15 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (v.geom[qt].bn == 0)
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s does not implement w%da%d (quant type not supported)",
                 idx, v.name, p.w_bits, p.a_bits);
+  const bool silu = (p.fmt & MXMOE_GG_EPI_SILU_MUL) != 0;
+  if (p.fmt & ~(0xFF | MXMOE_GG_EPI_SILU_MUL)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: unknown fmt flags %#x", idx, p.fmt);
+  if (silu && !(qt == QT_F16 || qt == QT_I8 || qt == QT_I4))
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: the SiLU epilogue needs fp16, w8a8_g-1_sym or w4a4_g-1_sym", idx);
+  if (silu && v.kind != Kind::V2 && v.kind != Kind::V3)
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s has no SiLU epilogue", idx, v.name);
+  if (silu && (v.persistent || v.geom[qt].bm != 256))
+    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s has no SiLU epilogue", idx, v.name);
+  if (silu && p.N % 32) return fail(MXMOE_GG_ERR_INVALID, "problem %d: the SiLU epilogue needs N %% 32 == 0 (N=%d)", idx, p.N);
   if (is_weightonly(qt)) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
   const int abits = is_float16(qt) ? 16 : p.a_bits;
   const int64_t kbits = (int64_t)p.K * abits;  // (fp6 images: K of the int4 codes they encode)
@@ -683,13 +693,15 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
 #endif
   const int64_t lda_b = p.lda ? p.lda * 2 : kbytes;
   const int64_t ldb_b = p.ldb ? p.ldb * 2 : kbytes;
-  const int64_t ldc = p.ldc ? p.ldc : p.N;
+  const int64_t ncols = silu ? p.N / 2 : p.N;  // columns of C
+  const int64_t ldc = p.ldc ? p.ldc : ncols;
   if (lda_b < kbytes || ldb_b < kbytes || (lda_b % 16) || (ldb_b % 16))
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: lda/ldb must be >= K row and a multiple of 8 words", idx);
   // the buffer-form LDS-DMA addresses a 256-row tile with 32-bit offsets below 2^31
   if (lda_b >= (int64_t)1 << 23 || ldb_b >= (int64_t)1 << 23)
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: A / B row strides must be below 8 MiB", idx);
-  if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
+  if (ldc < ncols || (ldc % 8))
+    return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= %s and a multiple of 8", idx, silu ? "N / 2" : "N");
   if (check_ptrs && p.M > 0 && p.N > 0) {  // empty problems are dropped by the planner
     if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
     if (!is_float16(qt) && (!p.SA || !p.SB)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer", idx);
@@ -706,6 +718,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   m->tiles_n = (p.N + v.geom[qt].bn - 1) / v.geom[qt].bn;
   m->kbytes = (int32_t)kbytes;
   m->reserved = qt == QT_I4G ? p.K / 128 : 0;  // w4a4 g128: scale groups
+  m->reserved2 = silu ? META_SILU : 0;
   m->lda_b = lda_b;
   m->ldb_b = ldb_b;
   m->ldc = ldc;
@@ -1205,7 +1218,9 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   *out = variant_index(kDefaultVariantName);
   const int wo_mask = (1 << QT_W4A16) | (1 << QT_W8A16) | (1 << QT_W2A16);
   const int small_mask = wo_mask | (1 << QT_I8) | (1 << QT_F16) | (1 << QT_I4);
-  if (mask != 0 && (mask & ~small_mask) == 0) {
+  bool any_silu = false;  // the small-batch kernel has no SiLU epilogue
+  for (const HostProblem& p : hp) any_silu = any_silu || (p.fmt & MXMOE_GG_EPI_SILU_MUL) != 0;
+  if (mask != 0 && (mask & ~small_mask) == 0 && !any_silu) {
     // (w8a8 / fp16 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
     double wsum0 = 0, ksum = 0;
     int kmax = 0;

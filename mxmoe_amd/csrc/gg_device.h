@@ -53,8 +53,12 @@ struct GGMeta {
   int32_t reserved;    // weight-only: 64-K stages per scale group
   int64_t lda_b, ldb_b;  // row strides of A / B in bytes
   int64_t ldc;           // row stride of C in fp16 elements
-  int64_t reserved2;     // weight-only: 1 = sym codes
+  int64_t reserved2;     // weight-only: 1 = sym codes; fp16 / w8a8 / w4a4: META_SILU
 };
+// GGMeta::reserved2 bit of a problem whose epilogue writes act = silu(gate) * up (MXMOE_GG_EPI_SILU_MUL):
+// B rows interleaved in 16-row blocks (gate block b at rows 32 b, up block b at 32 b + 16), C has
+// N / 2 columns
+constexpr int64_t META_SILU = 2;
 static_assert(sizeof(GGMeta) == 64, "GGMeta must stay 64 bytes");
 
 // One output tile (32 B), host-built in dispatch order: tile b is run by workgroup b.
@@ -476,6 +480,23 @@ __device__ __forceinline__ uint2 scale_pack4f(const v4f& acc, _Float16 sa, uint2
   const uint32_t s23 = __builtin_bit_cast(uint32_t, sa2 * __builtin_bit_cast(h2_t, sbw.y));
   const h2_t lo = {(_Float16)mul_f32_f16lo(acc[0], s01), (_Float16)mul_f32_f16hi(acc[1], s01)};
   const h2_t hi = {(_Float16)mul_f32_f16lo(acc[2], s23), (_Float16)mul_f32_f16hi(acc[3], s23)};
+  return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+}
+// act = fp16(silu(f32 g) * f32 u) of 4 fp16 gate / up values, silu(g) = g * rcp(1 + exp2(-g log2 e))
+// with the hardware exp2 / reciprocal: the arithmetic of the MoE activation kernel
+// (moe_ops.hip act_quant_kernel, SiLU mode), so the fused epilogue's act is bit-identical to it
+__device__ __forceinline__ uint2 silu_mul4(uint2 g, uint2 u) {
+  const h2_t g01 = __builtin_bit_cast(h2_t, g.x), g23 = __builtin_bit_cast(h2_t, g.y);
+  const h2_t u01 = __builtin_bit_cast(h2_t, u.x), u23 = __builtin_bit_cast(h2_t, u.y);
+  const _Float16 gv[4] = {g01[0], g01[1], g23[0], g23[1]}, uv[4] = {u01[0], u01[1], u23[0], u23[1]};
+  _Float16 h[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float gf = (float)gv[c];
+    const float sg = gf * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(gf * -1.4426950408889634f));
+    h[c] = (_Float16)(sg * (float)uv[c]);
+  }
+  const h2_t lo = {h[0], h[1]}, hi = {h[2], h[3]};
   return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
 }
 __device__ __forceinline__ uint2 pack4_f16(const v4f& acc) {
@@ -1464,20 +1485,51 @@ __device__ __forceinline__ void gg_tile_v2(const GGMeta& mt, const uint8_t* __re
 #pragma unroll
     for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * e_g);
   }
+  auto pack_frag = [&](int i, int j, _Float16 sai) {
+    if constexpr (QT == QT_F16 || QT == QT_BF16) return pack4_f16(acc[i][j]);
+    else if constexpr (QT == QT_F8) return scale_pack4f(acc[i][j], sai, sbw[j]);
+    else return scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
+  };
   auto pack_row = [&](int i) {  // fragment row i (16 rows of the wave's sub-tile) -> LDS
     const int ml = i * 16 + e_r16;
     _Float16 sai = 0;
     if constexpr (qt_scaled(QT)) sai = sl[wm * Cfg::WTM + ml];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      uint2 pk;
-      if constexpr (QT == QT_F16 || QT == QT_BF16) pk = pack4_f16(acc[i][j]);
-      else if constexpr (QT == QT_F8) pk = scale_pack4f(acc[i][j], sai, sbw[j]);
-      else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
+      const uint2 pk = pack_frag(i, j, sai);
       const int q = 2 * j + (e_g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * 128 + ((q ^ (ml & 7)) << 4) + (e_g & 1) * 8) = pk;
     }
   };
+  if constexpr (QT == QT_F16 || QT == QT_I8 || QT == QT_I4) {
+    if ((mt.reserved2 & META_SILU) != 0) {
+      // fused SiLU: fragments 2 jp (gate) and 2 jp + 1 (up) hold the same 16 output columns; the
+      // wave's 32 output columns are staged as 64-B rows and stored 16 rows per instruction
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = i * 16 + e_r16;
+        _Float16 sai = 0;
+        if constexpr (qt_scaled(QT)) sai = sl[wm * Cfg::WTM + ml];
+#pragma unroll
+        for (int jp = 0; jp < FN / 2; ++jp) {
+          const uint2 h = silu_mul4(pack_frag(i, 2 * jp, sai), pack_frag(i, 2 * jp + 1, sai));
+          const int q = 2 * jp + (e_g >> 1);
+          *reinterpret_cast<uint2*>(reg + ml * 64 + ((q ^ (ml & 3)) << 4) + (e_g & 1) * 8) = h;
+        }
+      }
+      const int ocol0 = ncol0 / 2, NO = N / 2;
+      _Float16* const obase = C + (int64_t)mrow0 * mt.ldc + ocol0;
+      const bool onarrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;  // byte offsets < 2^30
+#pragma unroll 4
+      for (int it = 0; it < Cfg::WTM / 16; ++it) {
+        const int row = it * 16 + (e_lane >> 2), q = e_lane & 3;
+        const uint4 v = *reinterpret_cast<const uint4*>(reg + row * 64 + ((q ^ (row & 3)) << 4));
+        if (mrow0 + row < M && ocol0 + q * 8 < NO)
+          store_c16<(ABL & V2_PLAINST) ? 0 : 16>(obase, (int64_t)row * mt.ldc + q * 8, onarrow, v);
+      }
+      return;
+    }
+  }
   _Float16* const cbase = C + (int64_t)mrow0 * mt.ldc + ncol0;  // wave-uniform
   const bool narrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;  // byte offsets < 2^30
   // (a wave reads back only its own region: LDS keeps one wave's accesses in order)
@@ -1782,7 +1834,9 @@ __device__ __forceinline__ int swz64(int r) { return (0x78 >> (2 * ((r >> 2) & 3
 // Epilogue shared by v3 / v4: dequant (int paths) + fp16 rounding, per-wave LDS staging of the
 // WTM x WTN fp16 sub-tile in XOR-swizzled 16-B chunks, then 16-B row stores (coalesced along N).
 // Needs WTM * WTN * 2 bytes of LDS per wave at `lds` (the drained ring).
-template <class Cfg, int QT>
+// SILU: compile the fused SiLU epilogue in (v3 tiles; the weight-only tiles, which never carry the
+// flag, leave it out — its code cost their 3-WG/CU build a spill)
+template <class Cfg, int QT, bool SILU = true>
 __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>::type (&acc)[Cfg::FM][Cfg::FN],
                                             const _Float16* __restrict__ SA, const _Float16* __restrict__ SB,
                                             _Float16* __restrict__ C, int m0, int n0, uint8_t* lds) {
@@ -1802,6 +1856,39 @@ __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>:
 #pragma unroll
     for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(SB + min(ncol0 + j * 16 + 4 * g, N - 4));
   }
+  auto pack_frag = [&](int i, int j, _Float16 sai) {
+    if constexpr (QT == QT_F16) return pack4_f16(acc[i][j]);
+    else if constexpr (QT == QT_I4F6) return scale_pack4f(acc[i][j], sai, sbw[j]);
+    else return scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
+  };
+  if constexpr (SILU && (QT == QT_F16 || QT == QT_I8 || QT == QT_I4)) {
+    if ((mt.reserved2 & META_SILU) != 0) {  // fused SiLU (as gg_tile_v2): rows of WTN / 2 outputs
+      constexpr int ORB = Cfg::WTN, OCPR = ORB / 16;  // staged output row bytes, 16-B chunks per row
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = i * 16 + r16;
+        _Float16 sai = 0;
+        if constexpr (QT != QT_F16) sai = SA[min(mrow0 + ml, M - 1)];
+#pragma unroll
+        for (int jp = 0; jp < FN / 2; ++jp) {
+          const uint2 h = silu_mul4(pack_frag(i, 2 * jp, sai), pack_frag(i, 2 * jp + 1, sai));
+          const int q = 2 * jp + (g >> 1);
+          *reinterpret_cast<uint2*>(reg + ml * ORB + ((q ^ (ml & (OCPR - 1))) << 4) + (g & 1) * 8) = h;
+        }
+      }
+      constexpr int ORPI = 64 / OCPR;
+      const int ocol0 = ncol0 / 2, NO = N / 2;
+      _Float16* const obase = C + (int64_t)mrow0 * mt.ldc + ocol0;
+      const bool onarrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;
+#pragma unroll 4
+      for (int it = 0; it < Cfg::WTM / ORPI; ++it) {
+        const int row = it * ORPI + lane / OCPR, q = lane % OCPR;
+        const uint4 v = *reinterpret_cast<const uint4*>(reg + row * ORB + ((q ^ (row & (OCPR - 1))) << 4));
+        if (mrow0 + row < M && ocol0 + q * 8 < NO) store_c16(obase, (int64_t)row * mt.ldc + q * 8, onarrow, v);
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int ml = i * 16 + r16;
@@ -1809,10 +1896,7 @@ __device__ __forceinline__ void epilogue_v3(const GGMeta& mt, typename AccT<QT>:
     if constexpr (QT != QT_F16) sai = SA[min(mrow0 + ml, M - 1)];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      uint2 pk;
-      if constexpr (QT == QT_F16) pk = pack4_f16(acc[i][j]);
-      else if constexpr (QT == QT_I4F6) pk = scale_pack4f(acc[i][j], sai, sbw[j]);  // f32 acc = the int32 sum
-      else pk = scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
+      const uint2 pk = pack_frag(i, j, sai);  // (QT_I4F6: the f32 acc is the int32 sum)
       const int q = 2 * j + (g >> 1);
       *reinterpret_cast<uint2*>(reg + ml * RB + ((q ^ (ml & (CPR - 1))) << 4) + (g & 1) * 8) = pk;
     }
@@ -2646,7 +2730,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     lds_barrier();  // ring -> epilogue staging
   }
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
-  epilogue_v3<Cfg, QT_F16>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
+  epilogue_v3<Cfg, QT_F16, false>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
 }
 
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel

@@ -211,8 +211,12 @@ __device__ __forceinline__ float amax8(const h8_t& x) {
 // interleaving the chunks' dependency chains (v_exp / v_rcp latency, packed-math wait states). parts == 4: the workgroups from blk_shared on take one
 // wide shared row each, wave w its w-th run of 128-aligned columns (the per-token amax then crosses
 // the 4 waves through LDS), so routed and shared rows share one launch and one register budget.
-template <bool SILU, int MAXC>
+// MODE 0: quant_act (routed slot s gathers hidden[perm[s]], width K); 1: silu_mul_quant (slot rows
+// [gate | up] of the gate_up output); 2: quant_slots (slot rows already activated: the gate_up
+// GroupGEMM's fused SiLU epilogue, routed [T*topk][N], shared [T][Ns])
+template <int MODE, int MAXC>
 __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
+  constexpr bool SILU = MODE == 1;
   __shared__ float wave_amax[kThreads / 64];
   const int lane = threadIdx.x & 63;
   const bool split_row = a.parts > 1 && (int64_t)blockIdx.x >= a.blk_shared;  // workgroup-uniform
@@ -224,11 +228,15 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const _Float16* row_src;
   if (s < a.ntk) {
     e = a.sorted[s];
-    row_src = SILU ? a.src + s * 2 * (int64_t)a.N : a.src + (int64_t)a.perm[s] * a.K;
+    row_src = MODE == 1 ? a.src + s * 2 * (int64_t)a.N
+            : MODE == 2 ? a.src + s * (int64_t)a.N
+                        : a.src + (int64_t)a.perm[s] * a.K;
   } else {
     e = a.nseg - 1;
     const int64_t t = s - a.ntk;
-    row_src = SILU ? a.src_shared + t * 2 * (int64_t)a.Ns : a.src + t * a.K;
+    row_src = MODE == 1 ? a.src_shared + t * 2 * (int64_t)a.Ns
+            : MODE == 2 ? a.src_shared + t * (int64_t)a.Ns
+                        : a.src + t * a.K;
   }
   if (e < 0 || e >= a.nseg) return;  // invalid id: the slot was never routed (route ignores it)
   const mxmoe_moe_seg sg = a.segs[e];
@@ -371,27 +379,36 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 using namespace mxmoe;
 
 // registers sized to the widest row of the launch, in 512-element chunks (1408 -> 3, 2048 -> 4)
-template <bool SILU>
+template <int MODE>
 static void launch_act_w(const ActArgs& a, int maxw, hipStream_t st) {
   const int64_t blocks = a.parts > 1 ? a.blk_shared + (a.nslots - a.ntk)
                                      : (a.nslots - a.s0 + kThreads / 64 - 1) / (kThreads / 64);
   const dim3 grid((unsigned)blocks), block(kThreads);
   const int nc = (maxw + 511) / 512;
-  if (nc <= 1) hipLaunchKernelGGL((act_quant_kernel<SILU, 1>), grid, block, 0, st, a);
-  else if (nc <= 2) hipLaunchKernelGGL((act_quant_kernel<SILU, 2>), grid, block, 0, st, a);
-  else if (nc <= 3) hipLaunchKernelGGL((act_quant_kernel<SILU, 3>), grid, block, 0, st, a);
-  else if (nc <= 4) hipLaunchKernelGGL((act_quant_kernel<SILU, 4>), grid, block, 0, st, a);
-  else if (nc <= 6) hipLaunchKernelGGL((act_quant_kernel<SILU, 6>), grid, block, 0, st, a);
-  else if (nc <= 8) hipLaunchKernelGGL((act_quant_kernel<SILU, 8>), grid, block, 0, st, a);
-  else if (nc <= 12) hipLaunchKernelGGL((act_quant_kernel<SILU, 12>), grid, block, 0, st, a);
-  else if (nc <= 16) hipLaunchKernelGGL((act_quant_kernel<SILU, 16>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((act_quant_kernel<SILU, 32>), grid, block, 0, st, a);
+  if (nc <= 1) hipLaunchKernelGGL((act_quant_kernel<MODE, 1>), grid, block, 0, st, a);
+  else if (nc <= 2) hipLaunchKernelGGL((act_quant_kernel<MODE, 2>), grid, block, 0, st, a);
+  else if (nc <= 3) hipLaunchKernelGGL((act_quant_kernel<MODE, 3>), grid, block, 0, st, a);
+  else if (nc <= 4) hipLaunchKernelGGL((act_quant_kernel<MODE, 4>), grid, block, 0, st, a);
+  else if (nc <= 6) hipLaunchKernelGGL((act_quant_kernel<MODE, 6>), grid, block, 0, st, a);
+  else if (nc <= 8) hipLaunchKernelGGL((act_quant_kernel<MODE, 8>), grid, block, 0, st, a);
+  else if (nc <= 12) hipLaunchKernelGGL((act_quant_kernel<MODE, 12>), grid, block, 0, st, a);
+  else if (nc <= 16) hipLaunchKernelGGL((act_quant_kernel<MODE, 16>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((act_quant_kernel<MODE, 32>), grid, block, 0, st, a);
 }
 
 // slots [0, nslots): one launch; rows of different widths (routed [0, ntk), shared [ntk, nslots)):
 // one launch with each shared row split over a workgroup's 4 waves when a quarter of the shared row
 // fits the routed rows' register width, else two launches, each with the register row of its width
-static int launch_act(bool silu, ActArgs a, int64_t nslots, int w_routed, int w_shared, void* stream) {
+template <int MODE>
+static void launch_act_m(const ActArgs& a, int maxw, hipStream_t st) {
+  launch_act_w<MODE>(a, maxw, st);
+}
+static void launch_act_any(int mode, const ActArgs& a, int maxw, hipStream_t st) {
+  if (mode == 1) launch_act_m<1>(a, maxw, st);
+  else if (mode == 2) launch_act_m<2>(a, maxw, st);
+  else launch_act_m<0>(a, maxw, st);
+}
+static int launch_act(int mode, ActArgs a, int64_t nslots, int w_routed, int w_shared, void* stream) {
   if (nslots == 0) return MXMOE_GG_OK;
   a.parts = 1;
   a.blk_shared = 0;
@@ -401,8 +418,7 @@ static int launch_act(bool silu, ActArgs a, int64_t nslots, int w_routed, int w_
     a.blk_shared = (a.ntk + kThreads / 64 - 1) / (kThreads / 64);
     a.s0 = 0;
     a.nslots = nslots;
-    if (silu) launch_act_w<true>(a, w_routed, (hipStream_t)stream);
-    else launch_act_w<false>(a, w_routed, (hipStream_t)stream);
+    launch_act_any(mode, a, w_routed, (hipStream_t)stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "act_quant_kernel launch failed: %s", hipGetErrorString(e));
     return MXMOE_GG_OK;
@@ -411,13 +427,11 @@ static int launch_act(bool silu, ActArgs a, int64_t nslots, int w_routed, int w_
   a.s0 = 0;
   a.nslots = split ? a.ntk : nslots;
   const int w0 = split ? w_routed : (nslots > a.ntk ? (w_routed > w_shared ? w_routed : w_shared) : w_routed);
-  if (silu) launch_act_w<true>(a, w0, (hipStream_t)stream);
-  else launch_act_w<false>(a, w0, (hipStream_t)stream);
+  launch_act_any(mode, a, w0, (hipStream_t)stream);
   if (split) {
     a.s0 = a.ntk;
     a.nslots = nslots;
-    if (silu) launch_act_w<true>(a, w_shared, (hipStream_t)stream);
-    else launch_act_w<false>(a, w_shared, (hipStream_t)stream);
+    launch_act_any(mode, a, w_shared, (hipStream_t)stream);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MXMOE_GG_ERR_HIP, "act_quant_kernel launch failed: %s", hipGetErrorString(e));
@@ -450,7 +464,7 @@ int mxmoe_moe_quant_act(const void* hidden, int64_t T, int K, int topk, int with
     return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_quant_act: NULL or misaligned pointer (hidden / out need 16 B)");
   const ActArgs a{static_cast<const _Float16*>(hidden), static_cast<const _Float16*>(hidden), T * topk, 0, 0, K, 0, 0,
                   sorted_expert, perm_token, segs, nseg, static_cast<uint8_t*>(out), static_cast<_Float16*>(scales)};
-  return launch_act(false, a, T * topk + (with_shared ? T : 0), K, K, stream);
+  return launch_act(0, a, T * topk + (with_shared ? T : 0), K, K, stream);
 }
 
 int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64_t T, int topk, int N, int N_shared,
@@ -466,7 +480,23 @@ int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64
   const ActArgs a{static_cast<const _Float16*>(routed_in), static_cast<const _Float16*>(shared_in), T * topk, 0, 0, 0,
                   N, N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
                   static_cast<_Float16*>(scales)};
-  return launch_act(true, a, T * topk + (shared_in ? T : 0), N, shared_in ? N_shared : N, stream);
+  return launch_act(1, a, T * topk + (shared_in ? T : 0), N, shared_in ? N_shared : N, stream);
+}
+
+int mxmoe_moe_quant_slots(const void* routed_in, const void* shared_in, int64_t T, int topk, int N, int N_shared,
+                          const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg, void* out, void* scales,
+                          void* stream) {
+  if (T < 0 || topk <= 0 || nseg <= 0 || N <= 0 || N % 128 || N > kMaxWidth ||
+      (shared_in && (N_shared <= 0 || N_shared % 128 || N_shared > kMaxWidth)))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_quant_slots: widths must be multiples of 128 and <= %d (N=%d, "
+                "N_shared=%d)", kMaxWidth, N, N_shared);
+  if (T > 0 && (!routed_in || !sorted_expert || !segs || !out || !aligned16(routed_in) || !aligned16(out) ||
+                (shared_in && !aligned16(shared_in))))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_quant_slots: NULL or misaligned pointer (16 B)");
+  const ActArgs a{static_cast<const _Float16*>(routed_in), static_cast<const _Float16*>(shared_in), T * topk, 0, 0, 0,
+                  N, N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
+                  static_cast<_Float16*>(scales)};
+  return launch_act(2, a, T * topk + (shared_in ? T : 0), N, shared_in ? N_shared : N, stream);
 }
 
 int mxmoe_moe_combine(const void* y, const int32_t* inv_slot, const float* weights, const void* shared,

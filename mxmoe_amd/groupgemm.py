@@ -129,6 +129,9 @@ class Problem:
     lda: int = 0  # row strides in 16-bit words, 0 = dense
     ldb: int = 0
     ldc: int = 0
+    # fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL): B rows gate / up interleaved in 16-row blocks
+    # (interleave_gate_up), C [M, N/2] = silu(gate) * up — fp16 / w8a8 / w4a4, large-batch kernels
+    silu: bool = False
 
     def __post_init__(self):
         """Operand dtypes must match q's format: the C-ABI sees only bytes, so an fp16 operand
@@ -156,11 +159,26 @@ class Problem:
         return nat.GGProblemC(
             A=ptr(self.A), B=ptr(self.B), scale_a=ptr(self.scale_a), scale_b=ptr(self.scale_b), C=ptr(self.C),
             M=self.M, N=self.N, K=self.K, a_bits=self.q.a_bits, w_bits=self.q.w_bits, gsize=self.q.gsize,
-            sym=int(self.q.sym), fmt=self.q.fmt_code, lda=self.lda, ldb=self.ldb, ldc=self.ldc)
+            sym=int(self.q.sym), fmt=self.q.fmt_code | (nat.EPI_SILU_MUL if self.silu else 0), lda=self.lda,
+            ldb=self.ldb, ldc=self.ldc)
 
     @property
     def flops(self) -> int:
         return 2 * self.M * self.N * self.K
+
+
+def interleave_gate_up(w: torch.Tensor, scale: Optional[torch.Tensor] = None, rows_per_row: int = 1):
+    """Gate / up rows of a [2N, ...] gate_up weight (gate rows first, then up rows) reordered for the
+    fused SiLU epilogue: 16-row blocks alternating gate block b, up block b. ``rows_per_row``: rows of
+    ``w`` per weight row (1 for the [N][K] layouts here). Returns (w', scale') — scale (per row,
+    [2N]) permuted alike. Done once per weight, like the weight-only repack."""
+    n2 = w.shape[0] // rows_per_row
+    if n2 % 32:
+        raise ValueError("interleave_gate_up: 2N must be a multiple of 32")
+    n = n2 // 2
+    idx = torch.arange(n2, device=w.device).view(2, n // 16, 16).transpose(0, 1).reshape(-1)
+    w2 = w.view(n2, rows_per_row, *w.shape[1:]).index_select(0, idx).reshape(w.shape)
+    return w2, (None if scale is None else scale.index_select(0, idx))
 
 
 def registry() -> list[str]:

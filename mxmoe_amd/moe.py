@@ -175,11 +175,14 @@ def quant_act(hidden: torch.Tensor, r: Routing, qtags: Sequence[int], with_share
 
 
 def silu_mul_quant(routed: torch.Tensor, shared: Optional[torch.Tensor], r: Routing, qtags: Sequence[int],
-                   stream: Optional[torch.cuda.Stream] = None) -> ActBatch:
+                   stream: Optional[torch.cuda.Stream] = None, activated: bool = False) -> ActBatch:
     """act = silu(gate) * up of the gate_up outputs (routed [T*topk, 2N] in slot order, shared
-    [T, 2Ns]), quantised per expert for the down GroupGEMM."""
-    N = routed.shape[1] // 2
-    Ns = shared.shape[1] // 2 if shared is not None else 0
+    [T, 2Ns]), quantised per expert for the down GroupGEMM. ``activated``: the inputs already are
+    the activations (routed [T*topk, N], shared [T, Ns]: the gate_up GroupGEMM's fused SiLU
+    epilogue) and only the quantisation runs (mxmoe_moe_quant_slots)."""
+    div = 1 if activated else 2
+    N = routed.shape[1] // div
+    Ns = shared.shape[1] // div if shared is not None else 0
     nseg = r.E + (1 if shared is not None else 0)
     if len(qtags) != nseg:
         raise ValueError(f"need {nseg} quant tags, got {len(qtags)}")
@@ -187,10 +190,11 @@ def silu_mul_quant(routed: torch.Tensor, shared: Optional[torch.Tensor], r: Rout
     first = r.first_slot + ([r.T * r.topk] if shared is not None else [])
     widths = [N] * r.E + ([Ns] if shared is not None else [])
     segs, dsegs, out, scales = _make_segments(rows, first, widths, qtags, routed.device)
+    fn = nat.lib().mxmoe_moe_quant_slots if activated else nat.lib().mxmoe_moe_silu_mul_quant
+
     def launch(st=stream):
-        nat.check(nat.lib().mxmoe_moe_silu_mul_quant(_ptr(routed), _ptr(shared), r.T, r.topk, N, Ns,
-                                                     _ptr(r.sorted_expert), _ptr(dsegs), nseg, _ptr(out),
-                                                     _ptr(scales), _stream(st)))
+        nat.check(fn(_ptr(routed), _ptr(shared), r.T, r.topk, N, Ns, _ptr(r.sorted_expert), _ptr(dsegs), nseg,
+                     _ptr(out), _ptr(scales), _stream(st)))
 
     launch()
     b = ActBatch(out, scales, segs, list(qtags))
@@ -393,11 +397,16 @@ class ExpertWeights:
     K: int
 
 
-def prepare_weight(w: torch.Tensor, q: QParams) -> ExpertWeights:
-    """fp16 [N, K] -> the GroupGEMM's B operand for qcfg q (setup, once per weight)."""
+def prepare_weight(w: torch.Tensor, q: QParams, interleave: bool = False) -> ExpertWeights:
+    """fp16 [N, K] -> the GroupGEMM's B operand for qcfg q (setup, once per weight). interleave: a
+    gate_up weight ([gate; up] rows) reordered for the fused SiLU epilogue (interleave_gate_up; the
+    per-row scales follow their rows)."""
+    from .groupgemm import interleave_gate_up
     from .quantize import pack_weightonly_mi355x, pack_wxax, quant_rtn_sym, quant_weightonly
 
     N, K = w.shape
+    if interleave:
+        w = interleave_gate_up(w)[0]  # (per-row quantisation commutes with the row order)
     if not q.is_quant:
         return ExpertWeights(w.contiguous(), None, q, N, K)
     if q.is_weight_only:
@@ -414,15 +423,24 @@ class MoEFFN:
     gate_up, QParams of down) — the activation side (a_bits, gsize) of each QParams sets how the
     plumbing quantises that expert's input (qtag_of). Expert E (if given) is the shared expert."""
 
+    FUSE_QCFGS = ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym")  # gate_up qcfgs with the SiLU epilogue
+
     def __init__(self, gate_up: Sequence[torch.Tensor], down: Sequence[torch.Tensor],
-                 qcfg: Sequence[tuple[QParams, QParams]], num_routed: int):
+                 qcfg: Sequence[tuple[QParams, QParams]], num_routed: int, fuse_silu: bool = False):
+        """fuse_silu: the gate_up GroupGEMM writes act = silu(gate) * up straight from its epilogue
+        (MXMOE_GG_EPI_SILU_MUL; gate_up weights stored with gate / up rows interleaved in 16-row
+        blocks) and only the quantisation runs after it — bit-identical outputs, half the gate_up C
+        bytes and no separate SiLU pass. Needs every gate_up qcfg in FUSE_QCFGS and N, Ns % 128 == 0."""
         self.E = num_routed
         self.has_shared = len(gate_up) == num_routed + 1
         self.H = gate_up[0].shape[1]
         self.N = gate_up[0].shape[0] // 2
         self.Ns = gate_up[-1].shape[0] // 2 if self.has_shared else 0
         self.qcfg = list(qcfg)
-        self.w1 = [prepare_weight(w, q[0]) for w, q in zip(gate_up, qcfg)]
+        self.fuse_silu = fuse_silu
+        if fuse_silu and any(q[0].qcfg not in self.FUSE_QCFGS for q in qcfg):
+            raise ValueError(f"fuse_silu needs every gate_up qcfg in {self.FUSE_QCFGS}")
+        self.w1 = [prepare_weight(w, q[0], interleave=fuse_silu) for w, q in zip(gate_up, qcfg)]
         self.w2 = [prepare_weight(w, q[1]) for w, q in zip(down, qcfg)]
         self.tag1 = [qtag_of(q[0].a_bits, q[0].gsize) for q in qcfg]
         self.tag2 = [qtag_of(q[1].a_bits, q[1].gsize) for q in qcfg]
@@ -434,8 +452,9 @@ class MoEFFN:
         r = route(topk_ids, self.E)
         topk = r.topk
         a1 = quant_act(hidden, r, self.tag1, self.has_shared)
-        h1 = torch.empty(T * topk, 2 * self.N, dtype=torch.float16, device=dev)
-        h1s = torch.empty(T, 2 * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
+        f = 1 if self.fuse_silu else 2  # (fused: the gate_up call writes the N-wide activations)
+        h1 = torch.empty(T * topk, f * self.N, dtype=torch.float16, device=dev)
+        h1s = torch.empty(T, f * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
         probs = []
         for e, s in enumerate(a1.segs):
             if s.rows == 0:
@@ -443,9 +462,9 @@ class MoEFFN:
             w = self.w1[e]
             C = h1s if e == self.E else h1[s.first_slot:s.first_slot + s.rows]
             probs.append(Problem(A=a1.A(e), B=w.B, C=C, M=s.rows, N=w.N, K=w.K, q=w.q, scale_a=a1.scale(e),
-                                 scale_b=w.scale_b))
+                                 scale_b=w.scale_b, silu=self.fuse_silu))
         GroupGemm(probs, device=dev).launch()
-        a2 = silu_mul_quant(h1, h1s, r, self.tag2)
+        a2 = silu_mul_quant(h1, h1s, r, self.tag2, activated=self.fuse_silu)
         y = torch.empty(T * topk, self.H, dtype=torch.float16, device=dev)
         ys = torch.empty(T, self.H, dtype=torch.float16, device=dev) if self.has_shared else None
         probs = []
