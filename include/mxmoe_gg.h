@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define MXMOE_GG_ABI_VERSION 5  /* 5: QParams padding ignored, groupgemm_mxmoe_fmt */
+#define MXMOE_GG_ABI_VERSION 6  /* 5: QParams padding ignored, groupgemm_mxmoe_fmt; 6: MXMOE_GG_EPI_SILU_MUL */
 
 enum {
   MXMOE_GG_OK = 0,

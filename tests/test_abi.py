@@ -41,7 +41,7 @@ def test_struct_layouts():
 
 
 def test_abi_version_and_variants():
-    assert nat.lib().mxmoe_gg_abi_version() == 5
+    assert nat.lib().mxmoe_gg_abi_version() == 6
     vs = nat.list_variants()
     assert len(vs) == nat.variant_count() >= 1
     assert "w8a8_g-1_sym=TileConfig(" in vs[0]
