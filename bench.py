@@ -468,6 +468,8 @@ def main():
                     help="skip the single-GPU strong-scaling simulation and the as-reference timing (N=1 only)")
     ap.add_argument("--variant", type=int, default=-1, help="-1 = library's choice (MXMOE_GG_VARIANT_AUTO)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-moe-layer", action="store_true",
+                    help="skip extras.moe_layer (the qwen2_moe layer-11 MoE FFN step, unfused vs fused SiLU epilogue)")
     ap.add_argument("--dist-extras-all", action="store_true",
                     help="N > 1: also run the N-slice strong-scaling and EP weak-scaling extras (off by default: "
                          "the default N > 1 run exercises one RCCL path, the expert split)")
@@ -692,6 +694,20 @@ def main():
                                  algorithmic_MB=round(bb / 1e6, 1), peak_gbs=HBM_GBS)
             else:
                 extras[x].update(bound="mfma", roofline_frac=round(ff / (tt * 1e-3) / 1e12 / pk, 4), peak_tflops=pk)
+
+    if world == 1 and not args.no_moe_layer and CONFIGS[cfg].get("model", "qwen2_moe") == "qwen2_moe":
+        try:  # the MoE layer around the path: not part of value
+            from mxmoe_amd.moe import qwen2_layer_bench
+
+            extras["moe_layer"] = {
+                "what": "qwen2_moe layer-11 MoE FFN at bs 8192 (LP-1 mixed, random weights, routed histogram), planned "
+                        "launches (moe.PlannedForward): quant_act -> gate_up -> SiLU-mul + quant -> down -> combine, "
+                        "device us (median of alternating rounds); fused = the gate_up epilogue writes silu(g)*u "
+                        "(MXMOE_GG_EPI_SILU_MUL) and only the quantisation follows",
+                **qwen2_layer_bench(rounds=2, iters=20)}
+            torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001 - an extra must not sink the headline line
+            extras["moe_layer"] = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     if world == 1 and not args.no_scaling_sim:
         from mxmoe_amd.harness import build_layer_inputs as _bli, ep_scaling_sim, time_reference_abi

@@ -480,3 +480,93 @@ class MoEFFN:
         if return_intermediates:
             return out, dict(routing=r, a1=a1, h1=h1, h1s=h1s, a2=a2, y=y, ys=ys)
         return out
+
+
+class PlannedForward:
+    """MoEFFN.forward for a fixed routing with every launch planned once: the plumbing kernels
+    relaunch on the same buffers and both GroupGEMMs keep their plans (the device work of a serving
+    step whose routing shapes repeat; the host planning MoEFFN.forward redoes per call is left out).
+    ``stages`` maps stage name -> launch; calling the object runs them in order into ``out``."""
+
+    def __init__(self, layer: "MoEFFN", hidden: torch.Tensor, topk_ids: torch.Tensor, topk_weights: torch.Tensor):
+        dev = hidden.device
+        T = hidden.shape[0]
+        self.r = r = route(topk_ids, layer.E)
+        topk = r.topk
+        self.a1 = quant_act(hidden, r, layer.tag1, layer.has_shared)
+        f = 1 if layer.fuse_silu else 2
+        self.h1 = torch.empty(T * topk, f * layer.N, dtype=torch.float16, device=dev)
+        self.h1s = torch.empty(T, f * layer.Ns, dtype=torch.float16, device=dev) if layer.has_shared else None
+        p1 = []
+        for e, sg in enumerate(self.a1.segs):
+            if sg.rows:
+                w = layer.w1[e]
+                C = self.h1s if e == layer.E else self.h1[sg.first_slot:sg.first_slot + sg.rows]
+                p1.append(Problem(A=self.a1.A(e), B=w.B, C=C, M=sg.rows, N=w.N, K=w.K, q=w.q, scale_a=self.a1.scale(e),
+                                  scale_b=w.scale_b, silu=layer.fuse_silu))
+        self.g1 = GroupGemm(p1, device=dev)
+        self.a2 = silu_mul_quant(self.h1, self.h1s, r, layer.tag2, activated=layer.fuse_silu)
+        self.y = torch.empty(T * topk, layer.H, dtype=torch.float16, device=dev)
+        self.ys = torch.empty(T, layer.H, dtype=torch.float16, device=dev) if layer.has_shared else None
+        p2 = []
+        for e, sg in enumerate(self.a2.segs):
+            if sg.rows:
+                w = layer.w2[e]
+                C = self.ys if e == layer.E else self.y[sg.first_slot:sg.first_slot + sg.rows]
+                p2.append(Problem(A=self.a2.A(e), B=w.B, C=C, M=sg.rows, N=w.N, K=w.K, q=w.q, scale_a=self.a2.scale(e),
+                                  scale_b=w.scale_b))
+        self.g2 = GroupGemm(p2, device=dev)
+        self.out = torch.empty(T, layer.H, dtype=torch.float16, device=dev)
+        self.w = topk_weights.to(torch.float32).contiguous()
+        self.stages = {"quant_act": self.a1.relaunch, "gate_up": self.g1.launch, "act_quant": self.a2.relaunch,
+                       "down": self.g2.launch,
+                       "combine": lambda: combine_into(self.out, self.y, r.inv_slot, self.w, self.ys, topk)}
+
+    def __call__(self) -> torch.Tensor:
+        for fn in self.stages.values():
+            fn()
+        return self.out
+
+
+def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192) -> dict:
+    """qwen2_moe layer 11 (LP-1 mixed w4a4 + w8a8 qconfig, the committed routing histogram, random
+    weights) as planned MoE FFN steps, unfused vs the fused SiLU epilogue: per-stage and step device
+    times (median over alternating rounds, µs) and whether the two outputs are bit-identical."""
+    from .harness import time_launches
+    from .workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+
+    E, H = 60, 2048
+    layer = load_workload(qwen2_layer11_workload(bs, qconfig=mixed_qconfig_lp1()))["layer-11"]
+    N, Ns = layer["down"][0].K, layer["down"][-1].K
+    topk = 4
+    qcfg = [(QParams(a.a_bits, a.w_bits, a.gsize, a.sym), QParams(b.a_bits, b.w_bits, b.gsize, b.sym))
+            for a, b in zip(layer["gate_up"], layer["down"])]
+    counts = [s.M for s in layer["gate_up"][:E]]
+    counts[0] += bs * topk - sum(counts)  # the histogram's int() truncation
+    dev = "cuda"
+    g = torch.Generator().manual_seed(0)
+    ids = torch.repeat_interleave(torch.arange(E, dtype=torch.int32), torch.tensor(counts))
+    ids = ids[torch.randperm(ids.numel(), generator=g)].view(bs, topk).contiguous().to(dev)
+    gate_up = [((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.05).half().to(dev) for _ in range(E)]
+    gate_up.append(((torch.rand(2 * Ns, H, generator=g) * 2 - 1) * 0.05).half().to(dev))
+    down = [((torch.rand(H, N, generator=g) * 2 - 1) * 0.05).half().to(dev) for _ in range(E)]
+    down.append(((torch.rand(H, Ns, generator=g) * 2 - 1) * 0.05).half().to(dev))
+    hidden = ((torch.rand(bs, H, generator=g) * 2 - 1)).half().to(dev)
+    wts = torch.softmax(torch.rand(bs, topk, generator=g), dim=1).to(dev)
+    steps = {name: PlannedForward(MoEFFN(gate_up, down, qcfg, num_routed=E, fuse_silu=fuse), hidden, ids, wts)
+             for name, fuse in (("unfused", False), ("fused", True))}
+    del gate_up, down
+    for st in steps.values():
+        st()
+    torch.cuda.synchronize()
+    same = torch.equal(steps["unfused"].out.view(torch.int16), steps["fused"].out.view(torch.int16))
+    res = {n: {"step": []} | {k: [] for k in st.stages} for n, st in steps.items()}
+    for _ in range(rounds):
+        for n, st in steps.items():
+            res[n]["step"].append(time_launches(st, 5, iters)["median_ms"])
+            for k, fn in st.stages.items():
+                res[n][k].append(time_launches(fn, 3, iters)["median_ms"])
+    out = {n: {k: round(sorted(v)[len(v) // 2] * 1e3, 1) for k, v in d.items()} for n, d in res.items()}
+    out["bit_identical"] = bool(same)
+    out["speedup"] = round(out["unfused"]["step"] / out["fused"]["step"], 4)
+    return out
