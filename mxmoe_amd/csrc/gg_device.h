@@ -485,20 +485,18 @@ __device__ __forceinline__ uint2 scale_pack4f(const v4f& acc, _Float16 sa, uint2
 // act = fp16(silu(f32 g) * f32 u) of 4 fp16 gate / up values, silu(g) = g * rcp(1 + exp2(-g log2 e))
 // with the hardware exp2 / reciprocal: the arithmetic of the MoE activation kernel
 // (moe_ops.hip act_quant_kernel, SiLU mode), so the fused epilogue's act is bit-identical to it
-__device__ __forceinline__ uint2 silu_mul4(uint2 g, uint2 u) {
-  const h2_t g01 = __builtin_bit_cast(h2_t, g.x), g23 = __builtin_bit_cast(h2_t, g.y);
-  const h2_t u01 = __builtin_bit_cast(h2_t, u.x), u23 = __builtin_bit_cast(h2_t, u.y);
-  const _Float16 gv[4] = {g01[0], g01[1], g23[0], g23[1]}, uv[4] = {u01[0], u01[1], u23[0], u23[1]};
-  _Float16 h[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const float gf = (float)gv[c];
-    const float sg = gf * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(gf * -1.4426950408889634f));
-    h[c] = (_Float16)(sg * (float)uv[c]);
-  }
-  const h2_t lo = {h[0], h[1]}, hi = {h[2], h[3]};
-  return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+// (pairs in float2 vectors: the multiplies and the add issue as v_pk_mul_f32 / v_pk_add_f32 — the
+// same IEEE operations, so the same bits, at half the VALU of the scalar form)
+__device__ __forceinline__ uint32_t silu_mul2(uint32_t g, uint32_t u) {
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  const f2_t gf = __builtin_convertvector(__builtin_bit_cast(h2_t, g), f2_t);
+  const f2_t uf = __builtin_convertvector(__builtin_bit_cast(h2_t, u), f2_t);
+  const f2_t t = gf * f2_t{-1.4426950408889634f, -1.4426950408889634f};
+  const f2_t d = f2_t{1.0f, 1.0f} + f2_t{__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+  const f2_t sg = gf * f2_t{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(sg * uf, h2_t));
 }
+__device__ __forceinline__ uint2 silu_mul4(uint2 g, uint2 u) { return uint2{silu_mul2(g.x, u.x), silu_mul2(g.y, u.y)}; }
 __device__ __forceinline__ uint2 pack4_f16(const v4f& acc) {
   const h2_t lo = {(_Float16)acc[0], (_Float16)acc[1]}, hi = {(_Float16)acc[2], (_Float16)acc[3]};
   return uint2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
