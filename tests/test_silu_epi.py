@@ -179,3 +179,39 @@ def test_moe_ffn_fused_equals_unfused(gpu, T):
     assert torch.equal(o1.view(torch.int16), o2.view(torch.int16))
     with pytest.raises(ValueError, match="fuse_silu"):
         moe.MoEFFN(gu, dn, [(W4A4_G128, W8A8)] + qcfg[1:], num_routed=E, fuse_silu=True)
+
+
+@pytest.mark.gpu
+def test_planned_forward_graph_replay(gpu):
+    """moe.PlannedForward (every launch pre-planned: quant_act, fused gate_up, quant_slots, down,
+    combine) captured into one HIP graph: replays return the eager step's output bit for bit."""
+    T, topk, E, H, N, Ns = 512, 4, 6, 256, 384, 768
+    g = torch.Generator().manual_seed(31)
+    gate_up = [((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half().to(DEV) for _ in range(E)]
+    gate_up.append(((torch.rand(2 * Ns, H, generator=g) * 2 - 1) * 0.2).half().to(DEV))
+    down = [((torch.rand(H, N, generator=g) * 2 - 1) * 0.2).half().to(DEV) for _ in range(E)]
+    down.append(((torch.rand(H, Ns, generator=g) * 2 - 1) * 0.2).half().to(DEV))
+    qcfg = [(W8A8, W8A8), (W4A4, W8A8), (FP16, FP16), (W8A8, W4A4), (W4A4, W4A4), (W8A8, FP16), (W4A4, W8A8)]
+    layer = moe.MoEFFN(gate_up, down, qcfg, num_routed=E, fuse_silu=True)
+    ids = torch.topk(torch.rand(T, E, generator=g), topk, dim=1).indices.to(torch.int32).to(DEV)
+    wts = torch.softmax(torch.rand(T, topk, generator=g), dim=1).to(DEV)
+    h = ((torch.rand(T, H, generator=g) * 2 - 1) * 3).half().to(DEV)
+    step = moe.PlannedForward(layer, h, ids, wts)
+    eager = step().clone()
+    ref = layer.forward(h, ids, wts)
+    torch.cuda.synchronize()
+    assert torch.equal(eager.view(torch.int16), ref.view(torch.int16))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        step()  # warm the stream
+        torch.cuda.synchronize()
+        step.out.fill_(float("nan"))
+        with torch.cuda.graph(graph, stream=s):
+            step()
+    for _ in range(2):
+        step.out.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(step.out.view(torch.int16), eager.view(torch.int16))
