@@ -76,6 +76,15 @@ int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64
                              const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg, void* out,
                              void* scales, void* stream);
 
+/* mxmoe_moe_silu_mul_quant on a gate_up output computed with gate / up rows interleaved in 16-row
+ * blocks (MXMOE_GG_EPI_SILU_MUL's weight layout) but the plain epilogue: routed_in [T*topk][2 N],
+ * shared_in [T][2 N_shared], columns [32 b, 32 b + 16) = gate columns [16 b, 16 b + 16) and
+ * [32 b + 16, 32 b + 32) the matching up columns. Same arithmetic and outputs as
+ * mxmoe_moe_silu_mul_quant on the de-interleaved input (the small-batch form of a fused layer). */
+int mxmoe_moe_silu_mul_quant_il(const void* routed_in, const void* shared_in, int64_t T, int topk, int N,
+                                int N_shared, const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg,
+                                void* out, void* scales, void* stream);
+
 /* mxmoe_moe_silu_mul_quant's quantisation alone, for activations the gate_up GroupGEMM already
  * produced with its fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL, include/mxmoe_gg.h): routed_in fp16
  * [T*topk][N] in slot order, shared_in fp16 [T][N_shared] or NULL; same segments, outputs and limits.

@@ -89,7 +89,7 @@ EXPORTED_SYMBOLS = (
     "groupgemm_mxmoe", "groupgemm_mxmoe_fmt", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     "mxmoe_gg_plan_tiles",
     # include/mxmoe_moe.h (MoE-layer plumbing)
-    "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_quant_slots", "mxmoe_moe_combine",
+    "mxmoe_moe_route", "mxmoe_moe_quant_act", "mxmoe_moe_silu_mul_quant", "mxmoe_moe_silu_mul_quant_il", "mxmoe_moe_quant_slots", "mxmoe_moe_combine",
 )
 
 
@@ -157,9 +157,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.mxmoe_moe_quant_act.argtypes = [P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, P, c.c_int, P, P, P]
     lib.mxmoe_moe_silu_mul_quant.restype = c.c_int
     lib.mxmoe_moe_silu_mul_quant.argtypes = [P, P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, c.c_int, P, P, P]
-    if hasattr(lib, "mxmoe_moe_quant_slots"):  # (builds before round 5's fused SiLU epilogue lack it: A/B tools)
-        lib.mxmoe_moe_quant_slots.restype = c.c_int
-        lib.mxmoe_moe_quant_slots.argtypes = [P, P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, c.c_int, P, P, P]
+    for fn in ("mxmoe_moe_quant_slots", "mxmoe_moe_silu_mul_quant_il"):
+        if hasattr(lib, fn):  # (builds before round 5's fused SiLU epilogue lack them: A/B tools)
+            getattr(lib, fn).restype = c.c_int
+            getattr(lib, fn).argtypes = [P, P, c.c_int64, c.c_int, c.c_int, c.c_int, P, P, c.c_int, P, P, P]
     lib.mxmoe_moe_combine.restype = c.c_int
     lib.mxmoe_moe_combine.argtypes = [P, P, P, P, P, c.c_int64, c.c_int, c.c_int, P, P]
 

@@ -213,10 +213,12 @@ __device__ __forceinline__ float amax8(const h8_t& x) {
 // the 4 waves through LDS), so routed and shared rows share one launch and one register budget.
 // MODE 0: quant_act (routed slot s gathers hidden[perm[s]], width K); 1: silu_mul_quant (slot rows
 // [gate | up] of the gate_up output); 2: quant_slots (slot rows already activated: the gate_up
-// GroupGEMM's fused SiLU epilogue, routed [T*topk][N], shared [T][Ns])
+// GroupGEMM's fused SiLU epilogue, routed [T*topk][N], shared [T][Ns]); 3: silu_mul_quant on a
+// gate_up output whose gate / up columns alternate in 16-column blocks (the interleaved weights of
+// the fused epilogue, run through the plain epilogue: small-batch calls on wo3)
 template <int MODE, int MAXC>
 __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
-  constexpr bool SILU = MODE == 1;
+  constexpr bool SILU = MODE == 1 || MODE == 3;
   __shared__ float wave_amax[kThreads / 64];
   const int lane = threadIdx.x & 63;
   const bool split_row = a.parts > 1 && (int64_t)blockIdx.x >= a.blk_shared;  // workgroup-uniform
@@ -228,13 +230,13 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const _Float16* row_src;
   if (s < a.ntk) {
     e = a.sorted[s];
-    row_src = MODE == 1 ? a.src + s * 2 * (int64_t)a.N
+    row_src = (MODE == 1 || MODE == 3) ? a.src + s * 2 * (int64_t)a.N
             : MODE == 2 ? a.src + s * (int64_t)a.N
                         : a.src + (int64_t)a.perm[s] * a.K;
   } else {
     e = a.nseg - 1;
     const int64_t t = s - a.ntk;
-    row_src = MODE == 1 ? a.src_shared + t * 2 * (int64_t)a.Ns
+    row_src = (MODE == 1 || MODE == 3) ? a.src_shared + t * 2 * (int64_t)a.Ns
             : MODE == 2 ? a.src_shared + t * (int64_t)a.Ns
                         : a.src + t * a.K;
   }
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
   const int col0 = part * qw;
   const int width = split_row ? max(0, min(qw, sg.width - col0)) : sg.width;
   // (a wave whose quarter of a split row is empty keeps a valid address: the row's start)
-  const _Float16* const base = width > 0 ? row_src + col0 : row_src;
+  const _Float16* const base = width > 0 ? row_src + (MODE == 3 ? 2 * col0 : col0) : row_src;
 
   // every load of the row first (all in flight together), then the arithmetic
   h8_t x[MAXC];
@@ -258,11 +260,13 @@ __global__ __launch_bounds__(kThreads) void act_quant_kernel(ActArgs a) {
     const int idx = c * 512 + lane * 8;
     const bool in = idx < width;
     const int li = in ? idx : 0;
-    const uint4 xv = *reinterpret_cast<const uint4*>(base + li);
+    // (MODE 3: element e of the row sits at 2 (e & ~15) + (e & 15), its up value 16 further)
+    const int gi = MODE == 3 ? 2 * (li & ~15) + (li & 15) : li;
+    const uint4 xv = *reinterpret_cast<const uint4*>(base + gi);
     const uint4 z = {0, 0, 0, 0};
     x[c] = __builtin_bit_cast(h8_t, in ? xv : z);
     if constexpr (SILU) {
-      const uint4 uv = *reinterpret_cast<const uint4*>(base + upoff + li);
+      const uint4 uv = *reinterpret_cast<const uint4*>(base + (MODE == 3 ? gi + 16 : upoff + li));
       u[c] = __builtin_bit_cast(h8_t, in ? uv : z);
     }
   }
@@ -406,6 +410,7 @@ static void launch_act_m(const ActArgs& a, int maxw, hipStream_t st) {
 static void launch_act_any(int mode, const ActArgs& a, int maxw, hipStream_t st) {
   if (mode == 1) launch_act_m<1>(a, maxw, st);
   else if (mode == 2) launch_act_m<2>(a, maxw, st);
+  else if (mode == 3) launch_act_m<3>(a, maxw, st);
   else launch_act_m<0>(a, maxw, st);
 }
 static int launch_act(int mode, ActArgs a, int64_t nslots, int w_routed, int w_shared, void* stream) {
@@ -481,6 +486,22 @@ int mxmoe_moe_silu_mul_quant(const void* routed_in, const void* shared_in, int64
                   N, N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
                   static_cast<_Float16*>(scales)};
   return launch_act(1, a, T * topk + (shared_in ? T : 0), N, shared_in ? N_shared : N, stream);
+}
+
+int mxmoe_moe_silu_mul_quant_il(const void* routed_in, const void* shared_in, int64_t T, int topk, int N,
+                                int N_shared, const int32_t* sorted_expert, const mxmoe_moe_seg* segs, int nseg,
+                                void* out, void* scales, void* stream) {
+  if (T < 0 || topk <= 0 || nseg <= 0 || N <= 0 || N % 128 || N > kMaxWidth ||
+      (shared_in && (N_shared <= 0 || N_shared % 128 || N_shared > kMaxWidth)))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_silu_mul_quant_il: widths must be multiples of 128 and <= %d (N=%d, "
+                "N_shared=%d)", kMaxWidth, N, N_shared);
+  if (T > 0 && (!routed_in || !sorted_expert || !segs || !out || !aligned16(routed_in) || !aligned16(out) ||
+                (shared_in && !aligned16(shared_in))))
+    return fail(MXMOE_GG_ERR_INVALID, "mxmoe_moe_silu_mul_quant_il: NULL or misaligned pointer (16 B)");
+  const ActArgs a{static_cast<const _Float16*>(routed_in), static_cast<const _Float16*>(shared_in), T * topk, 0, 0, 0,
+                  N, N_shared, sorted_expert, nullptr, segs, nseg, static_cast<uint8_t*>(out),
+                  static_cast<_Float16*>(scales)};
+  return launch_act(3, a, T * topk + (shared_in ? T : 0), N, shared_in ? N_shared : N, stream);
 }
 
 int mxmoe_moe_quant_slots(const void* routed_in, const void* shared_in, int64_t T, int topk, int N, int N_shared,

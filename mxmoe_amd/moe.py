@@ -175,11 +175,14 @@ def quant_act(hidden: torch.Tensor, r: Routing, qtags: Sequence[int], with_share
 
 
 def silu_mul_quant(routed: torch.Tensor, shared: Optional[torch.Tensor], r: Routing, qtags: Sequence[int],
-                   stream: Optional[torch.cuda.Stream] = None, activated: bool = False) -> ActBatch:
+                   stream: Optional[torch.cuda.Stream] = None, activated: bool = False,
+                   interleaved: bool = False) -> ActBatch:
     """act = silu(gate) * up of the gate_up outputs (routed [T*topk, 2N] in slot order, shared
     [T, 2Ns]), quantised per expert for the down GroupGEMM. ``activated``: the inputs already are
     the activations (routed [T*topk, N], shared [T, Ns]: the gate_up GroupGEMM's fused SiLU
-    epilogue) and only the quantisation runs (mxmoe_moe_quant_slots)."""
+    epilogue) and only the quantisation runs (mxmoe_moe_quant_slots). ``interleaved``: the gate_up
+    output's gate / up columns alternate in 16-column blocks (the fused layout's weights through the
+    plain epilogue; mxmoe_moe_silu_mul_quant_il)."""
     div = 1 if activated else 2
     N = routed.shape[1] // div
     Ns = shared.shape[1] // div if shared is not None else 0
@@ -190,7 +193,8 @@ def silu_mul_quant(routed: torch.Tensor, shared: Optional[torch.Tensor], r: Rout
     first = r.first_slot + ([r.T * r.topk] if shared is not None else [])
     widths = [N] * r.E + ([Ns] if shared is not None else [])
     segs, dsegs, out, scales = _make_segments(rows, first, widths, qtags, routed.device)
-    fn = nat.lib().mxmoe_moe_quant_slots if activated else nat.lib().mxmoe_moe_silu_mul_quant
+    fn = (nat.lib().mxmoe_moe_quant_slots if activated else
+          nat.lib().mxmoe_moe_silu_mul_quant_il if interleaved else nat.lib().mxmoe_moe_silu_mul_quant)
 
     def launch(st=stream):
         nat.check(fn(_ptr(routed), _ptr(shared), r.T, r.topk, N, Ns, _ptr(r.sorted_expert), _ptr(dsegs), nseg,
@@ -426,21 +430,25 @@ class MoEFFN:
     FUSE_QCFGS = ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym")  # gate_up qcfgs with the SiLU epilogue
 
     def __init__(self, gate_up: Sequence[torch.Tensor], down: Sequence[torch.Tensor],
-                 qcfg: Sequence[tuple[QParams, QParams]], num_routed: int, fuse_silu: bool = False):
+                 qcfg: Sequence[tuple[QParams, QParams]], num_routed: int, fuse_silu: Optional[bool] = None):
         """fuse_silu: the gate_up GroupGEMM writes act = silu(gate) * up straight from its epilogue
         (MXMOE_GG_EPI_SILU_MUL; gate_up weights stored with gate / up rows interleaved in 16-row
         blocks) and only the quantisation runs after it — bit-identical outputs, half the gate_up C
-        bytes and no separate SiLU pass. Needs every gate_up qcfg in FUSE_QCFGS and N, Ns % 128 == 0."""
+        bytes and no separate SiLU pass (qwen2_moe layer step -6 %). Needs every gate_up qcfg in
+        FUSE_QCFGS. None (default): fuse whenever the qcfgs allow. A call AUTO would hand to the
+        small-batch kernel (which has no SiLU epilogue) runs the plain epilogue on the interleaved
+        weights and the interleaved-input SiLU pass instead — same outputs, wo3's speed."""
         self.E = num_routed
         self.has_shared = len(gate_up) == num_routed + 1
         self.H = gate_up[0].shape[1]
         self.N = gate_up[0].shape[0] // 2
         self.Ns = gate_up[-1].shape[0] // 2 if self.has_shared else 0
         self.qcfg = list(qcfg)
-        self.fuse_silu = fuse_silu
-        if fuse_silu and any(q[0].qcfg not in self.FUSE_QCFGS for q in qcfg):
+        eligible = all(q[0].qcfg in self.FUSE_QCFGS for q in qcfg)
+        if fuse_silu and not eligible:
             raise ValueError(f"fuse_silu needs every gate_up qcfg in {self.FUSE_QCFGS}")
-        self.w1 = [prepare_weight(w, q[0], interleave=fuse_silu) for w, q in zip(gate_up, qcfg)]
+        self.fuse_silu = eligible if fuse_silu is None else fuse_silu
+        self.w1 = [prepare_weight(w, q[0], interleave=self.fuse_silu) for w, q in zip(gate_up, qcfg)]
         self.w2 = [prepare_weight(w, q[1]) for w, q in zip(down, qcfg)]
         self.tag1 = [qtag_of(q[0].a_bits, q[0].gsize) for q in qcfg]
         self.tag2 = [qtag_of(q[1].a_bits, q[1].gsize) for q in qcfg]
@@ -452,19 +460,9 @@ class MoEFFN:
         r = route(topk_ids, self.E)
         topk = r.topk
         a1 = quant_act(hidden, r, self.tag1, self.has_shared)
-        f = 1 if self.fuse_silu else 2  # (fused: the gate_up call writes the N-wide activations)
-        h1 = torch.empty(T * topk, f * self.N, dtype=torch.float16, device=dev)
-        h1s = torch.empty(T, f * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
-        probs = []
-        for e, s in enumerate(a1.segs):
-            if s.rows == 0:
-                continue
-            w = self.w1[e]
-            C = h1s if e == self.E else h1[s.first_slot:s.first_slot + s.rows]
-            probs.append(Problem(A=a1.A(e), B=w.B, C=C, M=s.rows, N=w.N, K=w.K, q=w.q, scale_a=a1.scale(e),
-                                 scale_b=w.scale_b, silu=self.fuse_silu))
-        GroupGemm(probs, device=dev).launch()
-        a2 = silu_mul_quant(h1, h1s, r, self.tag2, activated=self.fuse_silu)
+        g1, h1, h1s, mode = self.gate_up_call(a1, T, topk, dev)
+        g1.launch()
+        a2 = silu_mul_quant(h1, h1s, r, self.tag2, activated=mode == "fused", interleaved=mode == "interleaved")
         y = torch.empty(T * topk, self.H, dtype=torch.float16, device=dev)
         ys = torch.empty(T, self.H, dtype=torch.float16, device=dev) if self.has_shared else None
         probs = []
@@ -482,6 +480,39 @@ class MoEFFN:
         return out
 
 
+def _gate_up_call(self: "MoEFFN", a1: ActBatch, T: int, topk: int, dev):
+    """The planned gate_up GroupGEMM of one call and its output buffers: (GroupGemm, h1, h1s, mode),
+    mode "plain" ([gate | up] columns), "fused" (the SiLU epilogue: N-wide activations) or
+    "interleaved" (fused-layout weights through the plain epilogue, for calls AUTO sends to the
+    small-batch kernel)."""
+    def problems(C_of, silu):
+        ps = []
+        for e, sg in enumerate(a1.segs):
+            if sg.rows:
+                w = self.w1[e]
+                ps.append(Problem(A=a1.A(e), B=w.B, C=C_of(e, sg), M=sg.rows, N=w.N, K=w.K, q=w.q,
+                                  scale_a=a1.scale(e), scale_b=w.scale_b, silu=silu))
+        return ps
+
+    mode = "plain"
+    if self.fuse_silu:
+        mode = "fused"
+        ph = torch.empty(0, dtype=torch.float16, device=dev)
+        probe = problems(lambda e, sg: ph, False)  # shapes only: AUTO's choice for the plain epilogue
+        arr = (nat.GGProblemC * max(len(probe), 1))(*[p.to_c() for p in probe])
+        v = nat.resolve_variant(arr, len(probe))
+        if nat.list_variants()[v].split()[1].startswith("wo3"):
+            mode = "interleaved"
+    f = 1 if mode == "fused" else 2
+    h1 = torch.empty(T * topk, f * self.N, dtype=torch.float16, device=dev)
+    h1s = torch.empty(T, f * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
+    ps = problems(lambda e, sg: h1s if e == self.E else h1[sg.first_slot:sg.first_slot + sg.rows], mode == "fused")
+    return GroupGemm(ps, device=dev), h1, h1s, mode
+
+
+MoEFFN.gate_up_call = _gate_up_call
+
+
 class PlannedForward:
     """MoEFFN.forward for a fixed routing with every launch planned once: the plumbing kernels
     relaunch on the same buffers and both GroupGEMMs keep their plans (the device work of a serving
@@ -494,18 +525,9 @@ class PlannedForward:
         self.r = r = route(topk_ids, layer.E)
         topk = r.topk
         self.a1 = quant_act(hidden, r, layer.tag1, layer.has_shared)
-        f = 1 if layer.fuse_silu else 2
-        self.h1 = torch.empty(T * topk, f * layer.N, dtype=torch.float16, device=dev)
-        self.h1s = torch.empty(T, f * layer.Ns, dtype=torch.float16, device=dev) if layer.has_shared else None
-        p1 = []
-        for e, sg in enumerate(self.a1.segs):
-            if sg.rows:
-                w = layer.w1[e]
-                C = self.h1s if e == layer.E else self.h1[sg.first_slot:sg.first_slot + sg.rows]
-                p1.append(Problem(A=self.a1.A(e), B=w.B, C=C, M=sg.rows, N=w.N, K=w.K, q=w.q, scale_a=self.a1.scale(e),
-                                  scale_b=w.scale_b, silu=layer.fuse_silu))
-        self.g1 = GroupGemm(p1, device=dev)
-        self.a2 = silu_mul_quant(self.h1, self.h1s, r, layer.tag2, activated=layer.fuse_silu)
+        self.g1, self.h1, self.h1s, self.mode = layer.gate_up_call(self.a1, T, topk, dev)
+        self.a2 = silu_mul_quant(self.h1, self.h1s, r, layer.tag2, activated=self.mode == "fused",
+                                 interleaved=self.mode == "interleaved")
         self.y = torch.empty(T * topk, layer.H, dtype=torch.float16, device=dev)
         self.ys = torch.empty(T, layer.H, dtype=torch.float16, device=dev) if layer.has_shared else None
         p2 = []

@@ -151,13 +151,21 @@ def test_quant_slots_equals_silu_mul_quant(gpu):
                  [moe.ACT_INT4_G128] * E + [moe.ACT_INT8]):
         a = moe.silu_mul_quant(routed, shared, r, tags)
         b = moe.silu_mul_quant(act_r, act_s, r, tags, activated=True)
+        # the interleaved-input pass on the same values with gate / up columns in alternating
+        # 16-column blocks (the fused layout through the plain epilogue)
+        c = moe.silu_mul_quant(interleave_gate_up(routed.t())[0].t().contiguous(),
+                               interleave_gate_up(shared.t())[0].t().contiguous(), r, tags, interleaved=True)
         torch.cuda.synchronize()
         assert torch.equal(a.out, b.out) and torch.equal(a.scales, b.scales), tags
+        assert torch.equal(a.out, c.out) and torch.equal(a.scales, c.scales), tags
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T", [200, 2048])
-def test_moe_ffn_fused_equals_unfused(gpu, T):
+@pytest.mark.parametrize("T,mode", [(60, "interleaved"), (200, "fused"), (2048, "fused")])
+def test_moe_ffn_fused_equals_unfused(gpu, T, mode):
+    """A fused-layout layer equals the plain one bit for bit; at T = 60 AUTO would send the plain
+    gate_up call to wo3, so the layer runs the interleaved weights through the plain epilogue and
+    the interleaved-input SiLU pass (mxmoe_moe_silu_mul_quant_il) instead."""
     topk, E, H, N, Ns = 4, 6, 256, 384, 768
     g = torch.Generator().manual_seed(21)
     gate_up = [((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half() for _ in range(E)]
@@ -166,8 +174,9 @@ def test_moe_ffn_fused_equals_unfused(gpu, T):
     down.append(((torch.rand(H, Ns, generator=g) * 2 - 1) * 0.2).half())
     qcfg = [(W8A8, W8A8), (W4A4, W8A8), (FP16, FP16), (W8A8, W4A4), (W4A4, W4A4_G128), (W8A8, FP16), (W4A4, W8A8)]
     gu, dn = [w.to(DEV) for w in gate_up], [w.to(DEV) for w in down]
-    plain = moe.MoEFFN(gu, dn, qcfg, num_routed=E)
-    fused = moe.MoEFFN(gu, dn, qcfg, num_routed=E, fuse_silu=True)
+    plain = moe.MoEFFN(gu, dn, qcfg, num_routed=E, fuse_silu=False)
+    fused = moe.MoEFFN(gu, dn, qcfg, num_routed=E)  # (default: fused when every gate_up qcfg allows)
+    assert fused.fuse_silu
     logits = torch.rand(T, E, generator=g)
     ids = torch.topk(logits, topk, dim=1).indices.to(torch.int32).to(DEV)
     wts = torch.softmax(torch.rand(T, topk, generator=g), dim=1).to(DEV)
@@ -177,6 +186,7 @@ def test_moe_ffn_fused_equals_unfused(gpu, T):
     torch.cuda.synchronize()
     assert torch.equal(m1["a2"].out, m2["a2"].out) and torch.equal(m1["a2"].scales, m2["a2"].scales)
     assert torch.equal(o1.view(torch.int16), o2.view(torch.int16))
+    assert moe.PlannedForward(fused, h, ids, wts).mode == mode
     with pytest.raises(ValueError, match="fuse_silu"):
         moe.MoEFFN(gu, dn, [(W4A4_G128, W8A8)] + qcfg[1:], num_routed=E, fuse_silu=True)
 
