@@ -57,6 +57,13 @@ def test_abi_validation_without_gpu():
     assert b"K % 128" in lib.mxmoe_gg_last_error()
     assert lib.mxmoe_moe_combine(None, None, None, None, None, 4, 2, 12, None, None) == nat.MXMOE_GG_ERR_INVALID
     assert lib.mxmoe_moe_route(None, 4, 2, 0, None, None, None, None, None) == nat.MXMOE_GG_ERR_INVALID
+    # the fused-SiLU companions (round 5): widths must be multiples of 128, pointers 16-B aligned
+    for fn in (lib.mxmoe_moe_quant_slots, lib.mxmoe_moe_silu_mul_quant_il, lib.mxmoe_moe_silu_mul_quant):
+        assert fn(None, None, 4, 2, 100, 0, None, None, 1, None, None, None) == nat.MXMOE_GG_ERR_INVALID
+        assert b"multiples of 128" in lib.mxmoe_gg_last_error()
+        assert fn(None, None, 4, 2, 128, 0, None, None, 1, None, None, None) == nat.MXMOE_GG_ERR_INVALID
+        assert b"NULL or misaligned" in lib.mxmoe_gg_last_error()
+        assert fn(None, None, 0, 2, 128, 0, None, None, 1, None, None, None) == nat.MXMOE_GG_OK  # T = 0: nothing
     assert ctypes.sizeof(nat.MoeSegC) == 32
 
 
