@@ -550,17 +550,23 @@ class PlannedForward:
         return self.out
 
 
-def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192) -> dict:
-    """qwen2_moe layer 11 (LP-1 mixed w4a4 + w8a8 qconfig, the committed routing histogram, random
-    weights) as planned MoE FFN steps, unfused vs the fused SiLU epilogue: per-stage and step device
-    times (median over alternating rounds, µs) and whether the two outputs are bit-identical."""
+def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192, model: str = "qwen2_moe") -> dict:
+    """qwen2_moe layer 11 (LP-1 mixed w4a4 + w8a8 qconfig, the committed routing histogram) — or
+    model="ds2": the DeepSeek-V2-Lite mixed layer of the bench (64 routed experts, top-6, the two
+    shared experts as one of twice the width) — with random weights, as planned MoE FFN steps,
+    unfused vs the fused SiLU epilogue: per-stage and step device times (median over alternating
+    rounds, µs) and whether the two outputs are bit-identical."""
     from .harness import time_launches
-    from .workload import load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+    from .workload import ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
 
-    E, H = 60, 2048
-    layer = load_workload(qwen2_layer11_workload(bs, qconfig=mixed_qconfig_lp1()))["layer-11"]
+    if model == "ds2":
+        layer = load_workload(ds2_workload(bs, qconfig=ds2_mixed_qconfig()))["layer-1"]
+    else:
+        layer = load_workload(qwen2_layer11_workload(bs, qconfig=mixed_qconfig_lp1()))["layer-11"]
+    E = len(layer["gate_up"]) - 1
+    H = layer["gate_up"][0].K
     N, Ns = layer["down"][0].K, layer["down"][-1].K
-    topk = 4
+    topk = max(1, round(sum(s.M for s in layer["gate_up"][:E]) / bs))
     qcfg = [(QParams(a.a_bits, a.w_bits, a.gsize, a.sym), QParams(b.a_bits, b.w_bits, b.gsize, b.sym))
             for a, b in zip(layer["gate_up"], layer["down"])]
     counts = [s.M for s in layer["gate_up"][:E]]

@@ -21,8 +21,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--model", default="qwen2_moe", choices=["qwen2_moe", "ds2"])
     args = ap.parse_args()
-    r = moe.qwen2_layer_bench(args.rounds, args.iters)
+    r = moe.qwen2_layer_bench(args.rounds, args.iters, model=args.model)
+    r["model"] = args.model
     print(json.dumps(r), flush=True)
     if not r["bit_identical"]:
         sys.exit(1)
