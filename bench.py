@@ -708,6 +708,13 @@ def main():
             torch.cuda.empty_cache()
         except Exception as e:  # noqa: BLE001 - an extra must not sink the headline line
             extras["moe_layer"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        try:  # the same on the DeepSeek-V2-Lite mixed layer (64 routed experts, top-6, merged shared experts)
+            from mxmoe_amd.moe import qwen2_layer_bench
+
+            extras["moe_layer_ds2"] = qwen2_layer_bench(rounds=2, iters=20, model="ds2")
+            torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001
+            extras["moe_layer_ds2"] = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     if world == 1 and not args.no_scaling_sim:
         from mxmoe_amd.harness import build_layer_inputs as _bli, ep_scaling_sim, time_reference_abi
