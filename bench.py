@@ -284,7 +284,8 @@ def ep_combine_step(cfg: str, dev, world: int, rank: int, steps: int, warmup: in
     dn = layer["down"]
     T = dn[-1].M
     topk = -(-sum(s.M for s in dn[:-1]) // T)
-    step = EPCombineStep(inp["gate_up"], inp["down"], world, rank, synthetic_routing([s.M for s in dn[:-1]], T, topk))
+    step = EPCombineStep(inp["gate_up"], inp["down"], world, rank, synthetic_routing([s.M for s in dn[:-1]], T, topk),
+                         variant=variant)
     stream = torch.cuda.current_stream(dev)
 
     def timed(fn):

@@ -43,7 +43,8 @@
 extern "C" {
 #endif
 
-#define MXMOE_GG_ABI_VERSION 6  /* 5: QParams padding ignored, groupgemm_mxmoe_fmt; 6: MXMOE_GG_EPI_SILU_MUL */
+#define MXMOE_GG_ABI_VERSION 7  /* 5: QParams padding ignored, groupgemm_mxmoe_fmt; 6: MXMOE_GG_EPI_SILU_MUL;
+                                 * 7: mxmoe_gg_variant_caps */
 
 enum {
   MXMOE_GG_OK = 0,
@@ -144,6 +145,15 @@ int mxmoe_gg_list_variants(char* buf, size_t n);
  * writes BM, BN, K-bytes-per-stage and threads per workgroup. */
 int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int32_t* bn, int32_t* bk_bytes,
                           int32_t* threads);
+
+/* Capability bits of a compiled variant (mxmoe_gg_variant_caps). */
+#define MXMOE_GG_CAP_SILU_MUL 1u /* plans problems carrying MXMOE_GG_EPI_SILU_MUL (the fused SiLU epilogue) */
+
+/* Capabilities of variant `variant` (an index, not AUTO): *caps = OR of MXMOE_GG_CAP_* bits. Lets a
+ * caller ask whether the kernel AUTO resolved to supports an epilogue before planning with it
+ * (the MoE layer routes small-batch gate_up calls, whose kernel has no SiLU epilogue, through the
+ * interleaved SiLU pass). No reference counterpart: the reference compiles one epilogue per kernel. */
+int mxmoe_gg_variant_caps(int variant, uint32_t* caps);
 
 /* Pass as `variant` to mxmoe_gg_workspace_size / _plan / _run: the library picks the variant
  * from the quant types present (the plan info records the concrete one). groupgemm_mxmoe uses it. */

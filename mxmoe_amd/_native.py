@@ -70,6 +70,8 @@ class GGProblemC(ctypes.Structure):
 
 
 VARIANT_AUTO = -1  # MXMOE_GG_VARIANT_AUTO
+CAP_SILU_MUL = 1  # MXMOE_GG_CAP_SILU_MUL (mxmoe_gg_variant_caps)
+ABI_VERSION = 7  # MXMOE_GG_ABI_VERSION this binding is written for (include/mxmoe_gg.h)
 
 
 class GGPlanInfo(ctypes.Structure):
@@ -85,7 +87,7 @@ class GGPlanInfo(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "mxmoe_gg_abi_version", "mxmoe_gg_last_error", "mxmoe_gg_variant_count", "mxmoe_gg_default_variant",
     "mxmoe_gg_list_variants",
-    "mxmoe_gg_variant_tile", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_rebind", "mxmoe_gg_forget_workspace", "mxmoe_gg_launch", "mxmoe_gg_run",
+    "mxmoe_gg_variant_tile", "mxmoe_gg_variant_caps", "mxmoe_gg_resolve_variant", "mxmoe_gg_workspace_size", "mxmoe_gg_plan", "mxmoe_gg_rebind", "mxmoe_gg_forget_workspace", "mxmoe_gg_launch", "mxmoe_gg_run",
     "groupgemm_mxmoe", "groupgemm_mxmoe_fmt", "mxmoe_gg_release_shim_workspaces", "mxmoe_gg_repack_weightonly", "mxmoe_gg_debug_trace",
     "mxmoe_gg_plan_tiles",
     # include/mxmoe_moe.h (MoE-layer plumbing)
@@ -125,8 +127,12 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   c.POINTER(GGPlanInfo)]
     lib.mxmoe_gg_rebind.restype = c.c_int
     lib.mxmoe_gg_rebind.argtypes = [c.POINTER(GGProblemC), c.c_int, c.POINTER(GGPlanInfo), c.c_void_p]
-    lib.mxmoe_gg_forget_workspace.restype = c.c_int
-    lib.mxmoe_gg_forget_workspace.argtypes = [c.c_void_p]
+    if hasattr(lib, "mxmoe_gg_forget_workspace"):  # (ABI 6+; older builds loaded by A/B tools lack it)
+        lib.mxmoe_gg_forget_workspace.restype = c.c_int
+        lib.mxmoe_gg_forget_workspace.argtypes = [c.c_void_p]
+    if hasattr(lib, "mxmoe_gg_variant_caps"):  # (ABI 7+)
+        lib.mxmoe_gg_variant_caps.restype = c.c_int
+        lib.mxmoe_gg_variant_caps.argtypes = [c.c_int, c.POINTER(c.c_uint32)]
     lib.mxmoe_gg_launch.restype = c.c_int
     lib.mxmoe_gg_launch.argtypes = [c.POINTER(GGPlanInfo), c.c_void_p]
     lib.mxmoe_gg_run.restype = c.c_int
@@ -175,12 +181,31 @@ def lib() -> ctypes.CDLL:
                 f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(hipcc --offload-arch=gfx950). There is no fallback path.")
         try:
-            _lib = ctypes.CDLL(str(path))
+            handle = ctypes.CDLL(str(path))
         except OSError as e:  # pragma: no cover - environment dependent
             raise NativeLibraryError(f"failed to load {path}: {e}") from e
-        _declare(_lib)
+        _check_abi(handle, path)
+        _declare(handle)
+        _lib = handle
         atexit.register(_release_shim)
     return _lib
+
+
+def _check_abi(handle: ctypes.CDLL, path: Path) -> None:
+    """The product library must carry the ABI this binding is written for (a stale or foreign .so
+    raises NativeLibraryError here, not an AttributeError or a mis-typed call later). A library
+    named by MXMOE_GG_LIB (the A/B tools' older or lab builds) may be older: the symbols added
+    since are bound only where present."""
+    try:
+        fn = handle.mxmoe_gg_abi_version
+    except AttributeError as e:
+        raise NativeLibraryError(f"{path} exports no mxmoe_gg_abi_version: not a libmxmoe_gg build") from e
+    fn.restype, fn.argtypes = ctypes.c_int, []
+    got = fn()
+    if got == ABI_VERSION or ("MXMOE_GG_LIB" in os.environ and 5 <= got < ABI_VERSION):
+        return
+    raise NativeLibraryError(f"{path} has ABI version {got}, this binding needs {ABI_VERSION}: rebuild it with "
+                             "`python -c 'import __graft_entry__ as g; g.build()'`")
 
 
 def _release_shim() -> None:
@@ -257,6 +282,14 @@ def variant_supports(variant: int, qcfg: str) -> bool:
         return True
     line = list_variants()[variant]
     return f" {variant_key(qcfg)}=TileConfig(" in line
+
+
+def variant_caps(variant: int) -> int:
+    """Capability bits (CAP_*) of a compiled variant (mxmoe_gg_variant_caps): e.g. whether it has the
+    fused SiLU epilogue."""
+    out = ctypes.c_uint32()
+    check(lib().mxmoe_gg_variant_caps(variant, ctypes.byref(out)))
+    return out.value
 
 
 def variant_tile(variant: int, a_bits: int, w_bits: int) -> dict:

@@ -23,11 +23,17 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wa
          "-I", str(ROOT / "include")]
 
 
+# the lab build also compiles the lab-only kernels' headers
+LAB_DEPS = DEPS + [CSRC / "gg_f6.h"]
+
+
 def needs_build(lib: Path = LIB) -> bool:
+    """True when `lib` is missing or older than any source it is built from (the lab library's
+    tests skip on a stale lab build: a binary HEAD does not produce must not pass for HEAD's)."""
     if not lib.exists():
         return True
     t = lib.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in DEPS)
+    return any(p.stat().st_mtime > t for p in (LAB_DEPS if lib == LAB_LIB else DEPS))
 
 
 def build(force: bool = False, verbose: bool = False, extra: list[str] | None = None, lab: bool = False,

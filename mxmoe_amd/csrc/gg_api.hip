@@ -391,6 +391,17 @@ typedef TileCfg<128, 128, 2, 2, 2> T128x128;
 typedef TileCfg<256, 128, 2, 2, 1> T256x128;
 typedef TileCfg<128, 256, 2, 2, 1> T128x256;
 
+// the fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL) lives in the 256-row fp16 / w8a8 / w4a4 tile bodies
+// of the v2 / v3 kernels (gg_tile_v2, epilogue_v3); the small-batch wo3 kernel and the persistent
+// lab kernels have none (mxmoe_gg_variant_caps reports it)
+bool has_silu_epilogue(const Variant& v) {
+  if (v.kind != Kind::V2 && v.kind != Kind::V3) return false;
+  if (v.persistent) return false;
+  for (int q : {QT_F16, QT_I8, QT_I4})
+    if (v.geom[q].bm != 256) return false;
+  return true;
+}
+
 // Production variants (libmxmoe_gg.so): every one computes correct results. The lab build
 // (-DMXMOE_LAB -> libmxmoe_gg_lab.so, tools only: `python -m mxmoe_amd.build --lab`) compiles the
 // v2 family only, with the timing ablations (abl_*, WRONG RESULTS by design) and the mainloop
@@ -666,9 +677,7 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
   if (p.fmt & ~(0xFF | MXMOE_GG_EPI_SILU_MUL)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: unknown fmt flags %#x", idx, p.fmt);
   if (silu && !(qt == QT_F16 || qt == QT_I8 || qt == QT_I4))
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: the SiLU epilogue needs fp16, w8a8_g-1_sym or w4a4_g-1_sym", idx);
-  if (silu && v.kind != Kind::V2 && v.kind != Kind::V3)
-    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s has no SiLU epilogue", idx, v.name);
-  if (silu && (v.persistent || v.geom[qt].bm != 256))
+  if (silu && !has_silu_epilogue(v))
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s has no SiLU epilogue", idx, v.name);
   if (silu && p.N % 32) return fail(MXMOE_GG_ERR_INVALID, "problem %d: the SiLU epilogue needs N %% 32 == 0 (N=%d)", idx, p.N);
   if (is_weightonly(qt)) return build_meta_weightonly(p, idx, qt, v, check_ptrs, m);
@@ -1377,6 +1386,13 @@ int mxmoe_gg_list_variants(char* buf, size_t n) {
     buf[c] = 0;
   }
   return (int)vs.size();
+}
+
+int mxmoe_gg_variant_caps(int variant, uint32_t* caps) {
+  if (!caps) return fail(MXMOE_GG_ERR_INVALID, "caps is NULL");
+  if (int st = check_variant(variant)) return st;
+  *caps = has_silu_epilogue(variants()[variant]) ? MXMOE_GG_CAP_SILU_MUL : 0u;
+  return MXMOE_GG_OK;
 }
 
 int mxmoe_gg_variant_tile(int variant, int a_bits, int w_bits, int32_t* bm, int32_t* bn, int32_t* bk_bytes,

@@ -304,12 +304,13 @@ XGMI_LINK_GBS = 64.0  # effective all-gather GB/s per xGMI link and direction (o
 CHUNK_OVERHEAD_MS = 0.015  # per extra chunk: two more launches + one more ragged finish per call
 
 
-def gather_ms_model(bytes_received: float, world: int) -> float:
+def gather_ms_model(bytes_received: float, world: int, link_gbs: float = XGMI_LINK_GBS) -> float:
     """Modelled all-gather time: on a fully connected node every rank receives each peer's shard over
-    its own xGMI link, so (world - 1) links carry the bytes in parallel."""
+    its own xGMI link, so (world - 1) links carry the bytes in parallel (link_gbs: effective GB/s per
+    link and direction — an assumption, never measured here: no 8-GPU run has happened)."""
     if world <= 1:
         return 0.0
-    return bytes_received / ((world - 1) * XGMI_LINK_GBS * 1e9) * 1e3
+    return bytes_received / ((world - 1) * link_gbs * 1e9) * 1e3
 
 
 def choose_chunks(t_compute_ms: float, t_gather_ms: float, max_chunks: int = 8,
@@ -685,7 +686,8 @@ class _null:
 COMBINE_GBS = 6000.0  # mxmoe_moe_combine's measured streaming rate (6.5 TB/s at bs 8192)
 
 
-def exchange_model(t_compute_ms: float, world: int, pad_elems: int, cplan: Optional[CombinePlan], H: int) -> dict:
+def exchange_model(t_compute_ms: float, world: int, pad_elems: int, cplan: Optional[CombinePlan], H: int,
+                   link_gbs: float = XGMI_LINK_GBS) -> dict:
     """Modelled N > 1 step of both exchanges from a rank's compute time (all in ms; links as in
     gather_ms_model):
       allgather:   north_star's form — every rank's per-expert down C all-gathered (EPLayerStep),
@@ -694,7 +696,7 @@ def exchange_model(t_compute_ms: float, world: int, pad_elems: int, cplan: Optio
                    token's owner, the combine there, all-gather of the combined [T, H] output;
       combine_sharded: the same without the final all-gather (the output stays token-sharded, the
                    layout a data-parallel consumer of the layer reads)."""
-    tg = gather_ms_model(2.0 * pad_elems * (world - 1), world)
+    tg = gather_ms_model(2.0 * pad_elems * (world - 1), world, link_gbs)
     c = choose_chunks(t_compute_ms, tg)
     lo, hi = sorted((t_compute_ms, tg))
     out = {"allgather": {"MB_received": round(2.0 * pad_elems * (world - 1) / 1e6, 1), "gather_ms": round(tg, 4),
@@ -704,11 +706,37 @@ def exchange_model(t_compute_ms: float, world: int, pad_elems: int, cplan: Optio
         a2a = max(b["all_to_all"])
         ag = max(b["allgather_out"])
         n_max = max(t1 - t0 for t0, t1 in cplan.token_range)
-        t_a2a = gather_ms_model(a2a, world)
-        t_ag = gather_ms_model(ag, world)
+        t_a2a = gather_ms_model(a2a, world, link_gbs)
+        t_ag = gather_ms_model(ag, world, link_gbs)
         t_comb = n_max * H * 2 * (cplan.topk + 2) / (COMBINE_GBS * 1e9) * 1e3
         out["combine"] = {"a2a_MB_received": round(a2a / 1e6, 1), "allgather_out_MB_received": round(ag / 1e6, 1),
                           "a2a_ms": round(t_a2a, 4), "combine_ms": round(t_comb, 4), "allgather_out_ms": round(t_ag, 4),
                           "step_ms": round(t_compute_ms + t_a2a + t_comb + t_ag, 4)}
         out["combine_sharded"] = {"step_ms": round(t_compute_ms + t_a2a + t_comb, 4)}
+    return out
+
+
+def link_gbs_for_speedup(t1_ms: float, t_compute_ms: float, world: int, pad_elems: int, cplan: Optional[CombinePlan],
+                         H: int, target: float = 3.5, forms=("allgather", "combine", "combine_sharded"),
+                         hi_gbs: float = 10000.0) -> dict:
+    """Per exchange form, the effective xGMI GB/s per link (and direction) at which exchange_model's
+    step reaches ``target`` x the one-GPU layer time t1_ms; None where even an infinitely fast link
+    cannot (compute + fixed costs alone miss the target). Bisection on the monotone step(link) —
+    what a SCALE run has to show per link for north_star's >= 3.5x at 8 GPUs."""
+    out = {}
+    for form in forms:
+        if form != "allgather" and cplan is None:
+            continue
+
+        def speedup(gbs: float) -> float:
+            return t1_ms / exchange_model(t_compute_ms, world, pad_elems, cplan, H, link_gbs=gbs)[form]["step_ms"]
+
+        if speedup(hi_gbs) < target:
+            out[form] = None
+            continue
+        lo, hi = 1e-3, hi_gbs
+        for _ in range(60):
+            mid = (lo * hi) ** 0.5
+            lo, hi = (mid, hi) if speedup(mid) < target else (lo, mid)
+        out[form] = round(hi, 1)
     return out

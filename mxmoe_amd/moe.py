@@ -453,6 +453,48 @@ class MoEFFN:
         self.tag1 = [qtag_of(q[0].a_bits, q[0].gsize) for q in qcfg]
         self.tag2 = [qtag_of(q[1].a_bits, q[1].gsize) for q in qcfg]
 
+    def gate_up_call(self, a1: ActBatch, T: int, topk: int, dev):
+        """The planned gate_up GroupGEMM of one call and its output buffers: (GroupGemm, h1, h1s, mode),
+        mode "plain" ([gate | up] columns), "fused" (the SiLU epilogue: N-wide activations) or
+        "interleaved" (fused-layout weights through the plain epilogue and the interleaved-input SiLU
+        pass, for calls whose kernel has no SiLU epilogue). The library decides: the variant AUTO
+        resolves the call's shapes to is asked for MXMOE_GG_CAP_SILU_MUL (mxmoe_gg_variant_caps), and
+        a fused plan the library still refuses (GGError UNSUPPORTED) falls back to "interleaved"."""
+        def problems(C_of, silu):
+            ps = []
+            for e, sg in enumerate(a1.segs):
+                if sg.rows:
+                    w = self.w1[e]
+                    ps.append(Problem(A=a1.A(e), B=w.B, C=C_of(e, sg), M=sg.rows, N=w.N, K=w.K, q=w.q,
+                                      scale_a=a1.scale(e), scale_b=w.scale_b, silu=silu))
+            return ps
+
+        def buffers(mode):
+            f = 1 if mode == "fused" else 2
+            h1 = torch.empty(T * topk, f * self.N, dtype=torch.float16, device=dev)
+            h1s = torch.empty(T, f * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
+            ps = problems(lambda e, sg: h1s if e == self.E else h1[sg.first_slot:sg.first_slot + sg.rows],
+                          mode == "fused")
+            return ps, h1, h1s
+
+        mode = "plain"
+        if self.fuse_silu:
+            ph = torch.empty(0, dtype=torch.float16, device=dev)
+            probe = problems(lambda e, sg: ph, False)  # shapes only: AUTO's choice for the plain epilogue
+            arr = (nat.GGProblemC * max(len(probe), 1))(*[p.to_c() for p in probe])
+            v = nat.resolve_variant(arr, len(probe))
+            mode = "fused" if nat.variant_caps(v) & nat.CAP_SILU_MUL else "interleaved"
+        if mode == "fused":
+            ps, h1, h1s = buffers(mode)
+            try:
+                return GroupGemm(ps, device=dev), h1, h1s, mode
+            except nat.GGError as e:
+                if e.status != nat.MXMOE_GG_ERR_UNSUPPORTED:
+                    raise
+                mode = "interleaved"
+        ps, h1, h1s = buffers(mode)
+        return GroupGemm(ps, device=dev), h1, h1s, mode
+
     def forward(self, hidden: torch.Tensor, topk_ids: torch.Tensor, topk_weights: torch.Tensor,
                 shared_w: Optional[torch.Tensor] = None, return_intermediates: bool = False):
         T = hidden.shape[0]
@@ -480,37 +522,6 @@ class MoEFFN:
         return out
 
 
-def _gate_up_call(self: "MoEFFN", a1: ActBatch, T: int, topk: int, dev):
-    """The planned gate_up GroupGEMM of one call and its output buffers: (GroupGemm, h1, h1s, mode),
-    mode "plain" ([gate | up] columns), "fused" (the SiLU epilogue: N-wide activations) or
-    "interleaved" (fused-layout weights through the plain epilogue, for calls AUTO sends to the
-    small-batch kernel)."""
-    def problems(C_of, silu):
-        ps = []
-        for e, sg in enumerate(a1.segs):
-            if sg.rows:
-                w = self.w1[e]
-                ps.append(Problem(A=a1.A(e), B=w.B, C=C_of(e, sg), M=sg.rows, N=w.N, K=w.K, q=w.q,
-                                  scale_a=a1.scale(e), scale_b=w.scale_b, silu=silu))
-        return ps
-
-    mode = "plain"
-    if self.fuse_silu:
-        mode = "fused"
-        ph = torch.empty(0, dtype=torch.float16, device=dev)
-        probe = problems(lambda e, sg: ph, False)  # shapes only: AUTO's choice for the plain epilogue
-        arr = (nat.GGProblemC * max(len(probe), 1))(*[p.to_c() for p in probe])
-        v = nat.resolve_variant(arr, len(probe))
-        if nat.list_variants()[v].split()[1].startswith("wo3"):
-            mode = "interleaved"
-    f = 1 if mode == "fused" else 2
-    h1 = torch.empty(T * topk, f * self.N, dtype=torch.float16, device=dev)
-    h1s = torch.empty(T, f * self.Ns, dtype=torch.float16, device=dev) if self.has_shared else None
-    ps = problems(lambda e, sg: h1s if e == self.E else h1[sg.first_slot:sg.first_slot + sg.rows], mode == "fused")
-    return GroupGemm(ps, device=dev), h1, h1s, mode
-
-
-MoEFFN.gate_up_call = _gate_up_call
 
 
 class PlannedForward:

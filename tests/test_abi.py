@@ -41,12 +41,50 @@ def test_struct_layouts():
 
 
 def test_abi_version_and_variants():
-    assert nat.lib().mxmoe_gg_abi_version() == 6
+    assert nat.lib().mxmoe_gg_abi_version() == nat.ABI_VERSION == 7
     vs = nat.list_variants()
     assert len(vs) == nat.variant_count() >= 1
     assert "w8a8_g-1_sym=TileConfig(" in vs[0]
     t = nat.variant_tile(0, 8, 8)
     assert t["BM"] > 0 and t["BN"] > 0 and t["threads"] % 64 == 0
+
+
+def test_variant_caps_silu_epilogue():
+    """mxmoe_gg_variant_caps (ABI 7): the general kernels (v2x, v3) carry the fused SiLU epilogue, the
+    small-batch wo3 kernel does not — what MoEFFN.gate_up_call asks instead of matching names."""
+    names = {ln.split()[1]: int(ln.split()[0]) for ln in nat.list_variants()}
+    for name, v in names.items():
+        caps = nat.variant_caps(v)
+        assert bool(caps & nat.CAP_SILU_MUL) == (not name.startswith("wo")), name
+    with pytest.raises(nat.GGError):
+        nat.variant_caps(len(names))
+
+
+def test_stale_library_abi_refused(monkeypatch):
+    """A library whose ABI version differs from the binding's raises NativeLibraryError at load (not an
+    AttributeError later); a library named by MXMOE_GG_LIB (the A/B tools' older builds) may be
+    older, down to ABI 5."""
+    class Fn:
+        def __init__(self, v):
+            self.v = v
+
+        def __call__(self):
+            return self.v
+
+    class Lib:
+        def __init__(self, v):
+            self.mxmoe_gg_abi_version = Fn(v)
+
+    monkeypatch.delenv("MXMOE_GG_LIB", raising=False)
+    nat._check_abi(Lib(nat.ABI_VERSION), nat.LIB_PATH)
+    with pytest.raises(nat.NativeLibraryError):
+        nat._check_abi(Lib(nat.ABI_VERSION - 1), nat.LIB_PATH)
+    monkeypatch.setenv("MXMOE_GG_LIB", "/elsewhere/libmxmoe_gg_old.so")
+    nat._check_abi(Lib(6), nat.LIB_PATH)
+    with pytest.raises(nat.NativeLibraryError):
+        nat._check_abi(Lib(nat.ABI_VERSION + 1), nat.LIB_PATH)
+    with pytest.raises(nat.NativeLibraryError):
+        nat._check_abi(object(), nat.LIB_PATH)
 
 
 def test_workspace_size_grows_with_tiles():

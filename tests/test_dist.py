@@ -412,3 +412,97 @@ def test_exchange_model_token_owner_beats_allgather_at_8():
     assert 1.053 / m["combine"]["step_ms"] >= 3.5
     assert m["combine_sharded"]["step_ms"] < m["combine"]["step_ms"] < m["allgather"]["step_ms"]
     assert m["combine"]["a2a_MB_received"] + m["combine"]["allgather_out_MB_received"] < 0.35 * m["allgather"]["MB_received"]
+
+
+class _FakeDeviceTensor:
+    """Stands in for a CUDA tensor on the CPU-only host: .is_cuda is True and any host staging
+    (.cpu()) fails the test, so the RCCL branch must pass it to the collective untouched."""
+
+    is_cuda = True
+
+    def cpu(self):
+        raise AssertionError("device tensor staged through host memory under a non-gloo backend")
+
+
+@pytest.mark.parametrize("backend", ["nccl", "mpi"])
+def test_collectives_pass_device_tensors_straight_to_rccl(monkeypatch, backend):
+    """under any backend but gloo (RCCL is torch's "nccl" on ROCm) _all_gather and
+    _all_to_all_rows hand the device tensors themselves to the collective — no host round trip; under
+    gloo with device tensors (the one-GPU rehearsal) they stage through host memory."""
+    import mxmoe_amd.dist as md
+
+    calls = []
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: backend)
+    monkeypatch.setattr(dist, "all_gather_into_tensor", lambda out, inp, group=None: calls.append(("ag", out, inp)))
+    monkeypatch.setattr(dist, "all_to_all_single",
+                        lambda out, inp, osp, isp, group=None: calls.append(("a2a", out, inp, osp, isp)))
+    out, inp = _FakeDeviceTensor(), _FakeDeviceTensor()
+    md._all_gather(out, inp)
+    md._all_to_all_rows(out, inp, [1, 2], [2, 1])
+    assert calls == [("ag", out, inp), ("a2a", out, inp, [1, 2], [2, 1])]
+
+
+def test_collectives_stage_device_tensors_under_gloo(monkeypatch):
+    """The gloo branch (device tensors, one-GPU rehearsal): the collective sees host tensors and the
+    result is copied back into the device output."""
+    import mxmoe_amd.dist as md
+
+    seen = []
+
+    class Dev:
+        is_cuda = True
+
+        def __init__(self, t):
+            self.t = t
+            self.shape = t.shape
+            self.dtype = t.dtype
+
+        def numel(self):
+            return self.t.numel()
+
+        def cpu(self):
+            return self.t.clone()
+
+        def copy_(self, src):
+            self.t.copy_(src)
+
+    def ag(out, inp, group=None):
+        seen.append(type(inp))
+        out.copy_(torch.cat([inp, inp]))
+
+    def a2a(out, inp, osp, isp, group=None):
+        seen.append(type(inp))
+        out.copy_(inp)
+
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: "gloo")
+    monkeypatch.setattr(dist, "all_gather_into_tensor", ag)
+    monkeypatch.setattr(dist, "all_to_all_single", a2a)
+    out, inp = Dev(torch.zeros(4)), Dev(torch.tensor([1.0, 2.0]))
+    md._all_gather(out, inp)
+    assert out.t.tolist() == [1.0, 2.0, 1.0, 2.0]
+    rows = Dev(torch.zeros(2, 3))
+    md._all_to_all_rows(rows, Dev(torch.ones(2, 3)), [2], [2])
+    assert rows.t.sum().item() == 6.0
+    assert seen == [torch.Tensor, torch.Tensor]
+
+
+def test_link_rate_for_3p5x_at_8():
+    """the per-link xGMI rate each exchange needs for 3.5x at N = 8 (round-4 per-rank
+    compute 0.168 ms, T1 1.053 ms): the modelled step at the solved rate sits on the target, the
+    per-expert all-gather needs several times the token-owner exchange's rate, and the token-sharded
+    output the least."""
+    from mxmoe_amd.dist import ep_combine_plan, exchange_model, link_gbs_for_speedup, synthetic_routing
+
+    layer = _layer()
+    gu, dn = layer["gate_up"], layer["down"]
+    routing = synthetic_routing([s.M for s in dn[:-1]], dn[-1].M, 4)
+    plan = ep_layer_plan(gu, dn, 8)
+    pad = max(ep_shard_elems(dn, it) for it in plan)
+    cp = ep_combine_plan(plan, dn, routing)
+    need = link_gbs_for_speedup(1.053, 0.168, 8, pad, cp, 2048)
+    assert need["combine_sharded"] < need["combine"] < need["allgather"]
+    for form, gbs in need.items():
+        step = exchange_model(0.168, 8, pad, cp, 2048, link_gbs=gbs)[form]["step_ms"]
+        assert 3.45 <= 1.053 / step <= 3.6, (form, gbs, step)
+    # below the compute bound no link rate suffices
+    assert link_gbs_for_speedup(1.053, 0.32, 8, pad, cp, 2048)["combine"] is None

@@ -129,7 +129,7 @@ def test_abi_qparams_padding_and_fmt_field():
     assert nat.MxmoeQParams.sym.offset == 12 and nat.MxmoeQParams.pad_.offset == 13
     assert ctypes.sizeof(nat.MxmoeQParams) == 16
     assert nat.GGProblemC.fmt.offset == nat.GGProblemC.sym.offset + 4
-    assert nat.lib().mxmoe_gg_abi_version() == 6
+    assert nat.lib().mxmoe_gg_abi_version() == nat.ABI_VERSION
 
 
 def _plan_error(probs, variant):
