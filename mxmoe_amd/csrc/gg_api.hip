@@ -28,6 +28,7 @@
 #ifdef MXMOE_LAB
 #include "gg_f6.h"   // lab-only fp6 w4a4 route: measured slower than the int4 path
 #include "gg_v2q.h"  // lab-only persistent kernel: not compiled into the product library
+#include "gg_v4.h"   // lab-only one-wave-per-SIMD 256 x 256 tile
 // lab-only operand format: w4a4_g-1_sym with A / B as fp6 images (mxmoe_gg_pack_f6, gg_f6.h)
 #define MXMOE_GG_FMT_F6 3
 #define MXMOE_GG_F6_ROW_BYTES(K) ((((int64_t)(K) + 127) / 128) * 96)
@@ -378,6 +379,27 @@ Variant make_v2q(const char* name, int persist_len = 0) {
   v.persist_len = persist_len;
   return v;
 }
+// v4d (gg_v4.h): 256 x 256 tiles (+ 128 / 64-row classes), 4 waves at one per SIMD, fp16 / w8a8 only
+template <int QM>
+void launch_v4_q(const GGArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gg_v4_kernel<QM>), dim3(grid), dim3(256), 0, s, a);
+}
+void launch_v4(const GGArgs& a, int grid, int qmask, hipStream_t s) {
+  switch (qmask & 511) {
+    case 1: launch_v4_q<1>(a, grid, s); break;
+    case 2: launch_v4_q<2>(a, grid, s); break;
+    default: launch_v4_q<3>(a, grid, s); break;
+  }
+}
+Variant make_v4(const char* name) {
+  Variant v = v2_base(name, V4Cfg<256>::LDS_BYTES);
+  for (int q = 0; q < QT_COUNT; ++q)
+    if (q != QT_F16 && q != QT_I8) v.geom[q] = {0, 0, 0, 0};
+  v.geom[QT_F16].threads = v.geom[QT_I8].threads = 256;
+  v.threads = 256;
+  v.launch = &launch_v4;
+  return v;
+}
 #endif  // MXMOE_LAB
 
 // the small-batch weight-only tile's loop options (gg_tile_wo)
@@ -433,6 +455,7 @@ const std::vector<Variant>& variants() {
       // fast lab build (`python -m mxmoe_amd.build --lab-fast`): the product default and the
       // experiments under test only, fp16 / w8a8 bodies only
       make_v2<kV2x>("x_v2x"),
+      make_v4("x_v4d_256x256_w4_1wave"),
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),
@@ -1006,13 +1029,116 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
         all_tiles.push_back(td);
       }
   };
-  if (!regions_last) put_regions();
   const int TS = (int)seq.size();
+  // XCD packing (lab A/B: MXMOE_GG_XCD_PACK = 1 region tiles at the queue head,
+  // 2 at the tail). A call with region problems (the shared expert) and small ones (routed experts):
+  // every small problem goes WHOLE to one XCD — LPT over the problems' modelled loads, so its A / B
+  // panels live in one L2 — and the region problems' tiles, taken in rectangle order, are the filler
+  // that levels the XCDs: tile by tile to the XCD of least modelled load, then cut into consecutive
+  // pieces (XCD x's piece overlaps its rectangle, so the panel reuse of the rectangles is kept).
+  const char* pack_env = planner_knob("MXMOE_GG_XCD_PACK");
+  const int pack = pack_env ? atoi(pack_env) : 0;
+  bool packed = false;
+  if (pack > 0 && T_head > 0 && v.kind == Kind::V2 && !v.persistent) {
+    std::vector<std::pair<int, int>> runs;  // [s0, s1) of one problem's tiles in seq
+    for (int s0 = 0; s0 < TS; s0 = seq_end[s0]) runs.push_back({s0, seq_end[s0]});
+    std::vector<double> rl(runs.size(), 0.0);
+    for (size_t r = 0; r < runs.size(); ++r)
+      for (int s = runs[r].first; s < runs[r].second; ++s) rl[r] += tile_time(seq[s]);
+    std::vector<int> ro(runs.size());
+    for (size_t r = 0; r < ro.size(); ++r) ro[r] = (int)r;
+    std::stable_sort(ro.begin(), ro.end(), [&](int a, int b) { return rl[a] > rl[b]; });
+    double load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    std::vector<std::vector<int>> small_q(8);
+    for (int r : ro) {
+      int x = 0;
+      for (int y = 1; y < 8; ++y)
+        if (load[y] < load[x]) x = y;
+      load[x] += rl[r];
+      for (int s = runs[r].first; s < runs[r].second; ++s) small_q[x].push_back(s);
+    }
+    std::vector<TileDesc> big;
+    for (int x = 0; x < 8; ++x) big.insert(big.end(), region_tiles[x].begin(), region_tiles[x].end());
+    int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (const TileDesc& td : big) {
+      int x = 0;
+      for (int y = 1; y < 8; ++y)
+        if (load[y] < load[x]) x = y;
+      load[x] += tile_time(td);
+      ++cnt[x];
+    }
+    // the XCD's queue as its slots take it: region tiles first (pack 1) or last, and the queue's last
+    // 2 * chunk tiles longest first (the tail tiles of the routed bands are the short ones: LPT at the
+    // end evens the slots' finish; earlier tiles keep the band order)
+    auto build_q = [&](int x, size_t off, std::vector<int>* q) {
+      q->clear();
+      std::vector<int> bq;
+      for (int k = 0; k < cnt[x]; ++k) bq.push_back(-1 - (int)(off + k));  // (big tiles: -1 - index)
+      if (pack == 1) *q = bq;
+      q->insert(q->end(), small_q[x].begin(), small_q[x].end());
+      if (pack != 1) q->insert(q->end(), bq.begin(), bq.end());
+      const size_t n = q->size(), tail = std::min(n, (size_t)(2 * chunk));
+      auto tt = [&](int e) { return e < 0 ? tile_time(big[-1 - e]) : tile_time(seq[e]); };
+      std::stable_sort(q->end() - tail, q->end(), [&](int a, int b) { return tt(a) > tt(b); });
+    };
+    auto finish_of = [&](const std::vector<int>& q) {
+      XcdSim xs;
+      xs.slot.assign(chunk, 0.0);
+      for (int e : q) xs.add(e < 0 ? tile_time(big[-1 - e]) : tile_time(seq[e]));
+      return xs.finish;
+    };
+    // local search: move one region tile from the XCD that finishes last to the one that finishes
+    // first while the modelled makespan drops (the loads above are level; the slots' finish is not)
+    std::vector<std::vector<int>> q(8);
+    double fin[8];
+    auto rebuild = [&]() {
+      size_t off = 0;
+      for (int x = 0; x < 8; ++x) {
+        build_q(x, off, &q[x]);
+        fin[x] = finish_of(q[x]);
+        off += cnt[x];
+      }
+    };
+    rebuild();
+    // (compared as the sorted finish vector, latest first: a move that takes one of several XCDs off
+    // the makespan counts as a gain)
+    auto key = [&]() {
+      std::vector<double> f(fin, fin + 8);
+      std::sort(f.begin(), f.end(), std::greater<double>());
+      return f;
+    };
+    for (int it = 0; it < 128; ++it) {
+      int hi = 0, lo = 0;
+      for (int x = 1; x < 8; ++x) {
+        if (fin[x] > fin[hi]) hi = x;
+        if (fin[x] < fin[lo]) lo = x;
+      }
+      if (cnt[hi] == 0 || hi == lo) break;
+      const std::vector<double> before = key();
+      --cnt[hi];
+      ++cnt[lo];
+      rebuild();
+      if (!(key() < before)) {  // no gain: undo and stop
+        ++cnt[hi];
+        --cnt[lo];
+        rebuild();
+        break;
+      }
+    }
+    const int base = (int)all_tiles.size();
+    all_tiles.insert(all_tiles.end(), big.begin(), big.end());
+    for (int x = 0; x < 8; ++x) {
+      queue[x].clear();
+      for (int e : q[x]) queue[x].push_back(e < 0 ? base + (-1 - e) : e);
+    }
+    packed = true;
+  }
+  if (!regions_last && !packed) put_regions();
   const char* tc_env = planner_knob("MXMOE_GG_TAIL_CHUNK");  // A/B switch: tail chunk size (default 16)
   const int tail_chunk = tc_env && atoi(tc_env) > 0 ? atoi(tc_env) : 16;
   const char* rr_env = planner_knob("MXMOE_GG_XCD_RR");  // A/B switch: plain round-robin chunks
   const bool round_robin = rr_env && rr_env[0] == '1';
-  for (int s0 = 0, c = 0; s0 < TS; ++c) {
+  for (int s0 = 0, c = 0; s0 < TS && !packed; ++c) {
     const bool head = TS - s0 > 16 * chunk;
     int len = (round_robin || head) ? chunk : std::min(chunk, tail_chunk);
     if (head && !round_robin && align_on) {
@@ -1048,7 +1174,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     }
     s0 = s1;
   }
-  if (regions_last) put_regions();
+  if (regions_last && !packed) put_regions();
 
 #ifdef MXMOE_LAB
   // Tail split (v2, not persistent). An XCD hands its blocks to its CUs in queue order, so the
@@ -1129,6 +1255,34 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
         }
       }
       q.swap(q2);
+    }
+  }
+#endif
+#ifdef MXMOE_LAB
+  // Mixed residency (lab A/B, MXMOE_GG_MIX = 1): each XCD queue interleaved so a
+  // CU's co-resident workgroups (wo3: three) hold one full-height tile (a shared-expert tile, MFMA-
+  // heavy) beside the routed tiles of ~35 rows (weight-stream-heavy) instead of all-shared, then
+  // all-routed rounds: the routed tiles' stream then runs under the shared tiles' MFMAs. "Full" =
+  // a tile whose modelled time is at least 1.3x the queue's median.
+  const char* mix_env = planner_knob("MXMOE_GG_MIX");
+  if (mix_env && mix_env[0] == '1' && v.kind == Kind::V2 && !v.persistent) {
+    for (auto& q : queue) {
+      if (q.size() < 4) continue;
+      std::vector<double> t(q.size());
+      for (size_t j = 0; j < q.size(); ++j) t[j] = tile_time(all_tiles[q[j]]);
+      std::vector<double> srt(t);
+      std::nth_element(srt.begin(), srt.begin() + srt.size() / 2, srt.end());
+      const double med = srt[srt.size() / 2];
+      std::vector<int> lo, hi;
+      for (size_t j = 0; j < q.size(); ++j) ((t[j] >= 1.3 * med) ? hi : lo).push_back(q[j]);
+      if (hi.empty() || lo.empty()) continue;
+      std::vector<int> out;
+      size_t a = 0, b = 0;
+      while (a < hi.size() || b < lo.size()) {  // keep the hi : lo proportion along the queue
+        if (b >= lo.size() || (a < hi.size() && a * lo.size() <= b * hi.size())) out.push_back(hi[a++]);
+        else out.push_back(lo[b++]);
+      }
+      q.swap(out);
     }
   }
 #endif

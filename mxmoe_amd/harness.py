@@ -218,7 +218,8 @@ def ep_scaling_sim(gate_up: LayerInputs, down: LayerInputs, worlds: Sequence[int
     headline's plan), measured on ONE GPU: every rank's gate_up + down calls over its row items are
     timed as their own calls (ranks are independent GPUs); T_G = max over ranks, speedup = T_1 / T_G.
     The all-gather of the down outputs that follows on a node is listed as MB received per rank."""
-    from .dist import ep_combine_plan, ep_layer_plan, ep_shard_elems, exchange_model, synthetic_routing
+    from .dist import (XGMI_LINK_GBS, ep_combine_plan, ep_layer_plan, ep_shard_elems, exchange_model,
+                       link_gbs_for_speedup, synthetic_routing)
 
     def t_pair(gu, dn):
         ggs = [GroupGemm(x, variant=variant) for x in (gu, dn) if x]
@@ -243,7 +244,11 @@ def ep_scaling_sim(gate_up: LayerInputs, down: LayerInputs, worlds: Sequence[int
         out[str(G)] = {"t_ms_max_rank": round(tg, 4), "speedup": round(t1 / tg, 3),
                        "rank_ms": [round(x, 4) for x in rank_ms],
                        "allgather_MB_per_rank": round(2 * pad * (G - 1) / 1e6, 1),
-                       "modelled": {k: {**v, "speedup": round(t1 / v["step_ms"], 3)} for k, v in model.items()}}
+                       "modelled": {k: {**v, "speedup": round(t1 / v["step_ms"], 3)} for k, v in model.items()},
+                       # the effective GB/s per xGMI link (and direction) each exchange needs for 3.5x (None:
+                       # not reachable at any link rate); the model above assumes XGMI_LINK_GBS
+                       "link_GBs_for_3p5x": link_gbs_for_speedup(t1, tg, G, pad, cplan, H),
+                       "link_GBs_assumed": XGMI_LINK_GBS}
     return out
 
 
