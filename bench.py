@@ -403,13 +403,19 @@ def one_problem(a, b, sa, sb):
 
 
 def load_pmc_traffic(cfg: str):
+    """The committed counter bytes of `cfg` (profiles/pmc_traffic.json, tools/pmc_traffic.sh), with
+    `_source`: which round's tree measured them (the file's `_round` / per-config `_round` tags)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(cfg)
+        c = d.get(cfg)
+        if isinstance(c, dict):
+            rnd = c.get("_round", d.get("_round", "unknown round"))
+            c = {**c, "_source": f"profiles/pmc_traffic.json ({rnd}; FETCH_SIZE x2 + WRITE_SIZE per step)"}
+        return c
     except Exception:  # pragma: no cover
         return None
 
@@ -783,6 +789,7 @@ def main():
                        "variant_name": nat.list_variants()[main_res["variant"]].split()[1]},
             "roofline": {**roof,
                          "traffic": pmc.get("hbm_bytes_per_step") if isinstance(pmc, dict) else None,
+                         "traffic_source": pmc.get("_source") if isinstance(pmc, dict) else None,
                          "kernel": kernel_symbol(nat.list_variants()[main_res["variant"]].split()[1])
                          + " (gate_up + down launches; achieved = sum FLOPs / sum mean launch time)",
                          "launch_ms": {"gate_up": round(t_gu, 4), "down": round(t_dn, 4)}},

@@ -380,24 +380,26 @@ Variant make_v2q(const char* name, int persist_len = 0) {
   return v;
 }
 // v4d (gg_v4.h): 256 x 256 tiles (+ 128 / 64-row classes), 4 waves at one per SIMD, fp16 / w8a8 only
-template <int QM>
+template <int QM, int OPT>
 void launch_v4_q(const GGArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gg_v4_kernel<QM>), dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gg_v4_kernel<QM, OPT>), dim3(grid), dim3(256), 0, s, a);
 }
+template <int OPT = 0>
 void launch_v4(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {
-    case 1: launch_v4_q<1>(a, grid, s); break;
-    case 2: launch_v4_q<2>(a, grid, s); break;
-    default: launch_v4_q<3>(a, grid, s); break;
+    case 1: launch_v4_q<1, OPT>(a, grid, s); break;
+    case 2: launch_v4_q<2, OPT>(a, grid, s); break;
+    default: launch_v4_q<3, OPT>(a, grid, s); break;
   }
 }
+template <int OPT = 0>
 Variant make_v4(const char* name) {
   Variant v = v2_base(name, V4Cfg<256>::LDS_BYTES);
   for (int q = 0; q < QT_COUNT; ++q)
     if (q != QT_F16 && q != QT_I8) v.geom[q] = {0, 0, 0, 0};
   v.geom[QT_F16].threads = v.geom[QT_I8].threads = 256;
   v.threads = 256;
-  v.launch = &launch_v4;
+  v.launch = &launch_v4<OPT>;
   return v;
 }
 #endif  // MXMOE_LAB
@@ -456,6 +458,7 @@ const std::vector<Variant>& variants() {
       // experiments under test only, fp16 / w8a8 bodies only
       make_v2<kV2x>("x_v2x"),
       make_v4("x_v4d_256x256_w4_1wave"),
+      make_v4<1>("abl_v4d_stamp"),
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),
@@ -484,6 +487,11 @@ const std::vector<Variant>& variants() {
       make_v2<kV2x>("x_v2x"),
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_I4NOPAIR | V2_I4EDMA>("x_v2x_i4edma"),
+      // the product's default and small-batch kernels, for planner A/B runs (MXMOE_GG_XCD_PACK, _MIX)
+      make_v2<kV2x | WO_PIPE | WO_STAG | V2_I4NOPAIR | V2_I4EDMA>("x_v2x_product"),
+      make_wo2<kWo3, 3>("x_wo3"),
+      // round 6: v4d, one wave per SIMD (gg_v4.h; fp16 / w8a8)
+      make_v4("x_v4d_256x256_w4_1wave"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_EPIPE>("x_v2x_epipe"),
       make_v2<kV2x | V2_LATEIL>("x_v2x_lateil"),
@@ -559,6 +567,9 @@ constexpr double kWoSmallMeanRows = 512.0;
 constexpr double kSmallMeanRows = 80.0;
 constexpr double kSmallMeanRowsI4 = 112.0;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
+// XCD packing (plan_host): region tiles at the queue head for calls below this many flops per
+// algorithmic byte (qwen2_moe layer 11: fp16 524-593, w8a8 849-919, mixed 987-1193, w4a4 1233-1268)
+constexpr double kPackHeadFlopPerByte = 700.0;
 
 int variant_index(const char* name) {
   for (size_t i = 0; i < variants().size(); ++i)
@@ -934,7 +945,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     }
     return out->gm != 0;
   };
-  int groups = 0;
+  int groups = 0, n_region = 0;
   std::vector<TileDesc> seq;                // chunked tiles
   std::vector<int> seq_end;                 // per seq tile: end of its problem's run in seq
   std::vector<std::vector<TileDesc>> region_tiles(8);  // per XCD
@@ -946,6 +957,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     const int nt = m.tiles_n, S = split[order[row]], nst = stages_of(m);
     Region rg;
     if (region_of(order[row], &rg)) {
+      ++n_region;
       for (int x = 0; x < 8; ++x) {
         const int mb0 = (x / rg.gn) * rg.r, mb1 = std::min((int)mt.size(), mb0 + rg.r);
         const int nb0 = (x % rg.gn) * rg.c, nb1 = std::min(nt, nb0 + rg.c);
@@ -1036,10 +1048,20 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // panels live in one L2 — and the region problems' tiles, taken in rectangle order, are the filler
   // that levels the XCDs: tile by tile to the XCD of least modelled load, then cut into consecutive
   // pieces (XCD x's piece overlaps its rectangle, so the panel reuse of the rectangles is kept).
+  // Default (pack 4, product): packing for the MoE call shape — ONE region problem (the shared expert)
+  // beside >= 8 whole small problems — with the region tiles at the queue head when they are the long
+  // ones (down: K 4x the routed K; LPT) or when the call streams many bytes per flop (arithmetic
+  // intensity under kPackHeadFlopPerByte: the 16-bit calls, whose head placement cut the fp16 gate_up
+  // counter bytes 2.97 -> 2.35 GB and ran 2.4 % faster, where w8a8 gate_up at the head ran 4 % slower
+  // (profiles/r06/pack/)); every other call keeps the chunked placement below. Lab A/B:
+  // MXMOE_GG_XCD_PACK = 0 off, 1 always head, 2 always tail, 3 head only for long region tiles.
   const char* pack_env = planner_knob("MXMOE_GG_XCD_PACK");
-  const int pack = pack_env ? atoi(pack_env) : 0;
+  const int pack = pack_env ? atoi(pack_env) : 4;
   bool packed = false;
-  if (pack > 0 && T_head > 0 && v.kind == Kind::V2 && !v.persistent) {
+  int n_small = 0;
+  for (int s0 = 0; s0 < TS; s0 = seq_end[s0]) ++n_small;
+  const bool moe_shape = n_region == 1 && n_small >= 8;
+  if (pack > 0 && T_head > 0 && v.kind == Kind::V2 && !v.persistent && (pack != 4 || moe_shape)) {
     std::vector<std::pair<int, int>> runs;  // [s0, s1) of one problem's tiles in seq
     for (int s0 = 0; s0 < TS; s0 = seq_end[s0]) runs.push_back({s0, seq_end[s0]});
     std::vector<double> rl(runs.size(), 0.0);
@@ -1070,13 +1092,48 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     // the XCD's queue as its slots take it: region tiles first (pack 1) or last, and the queue's last
     // 2 * chunk tiles longest first (the tail tiles of the routed bands are the short ones: LPT at the
     // end evens the slots' finish; earlier tiles keep the band order)
-    auto build_q = [&](int x, size_t off, std::vector<int>* q) {
+    // pack 3: at the head when the region tiles are the long ones (the down call's shared expert, 4x
+    // the routed K: LPT), at the tail otherwise (gate_up: every tile the same length)
+    bool head = pack == 1;
+    if (pack >= 3) {
+      double tb = 0, ts = 0;
+      for (const TileDesc& td : big) tb += tile_time(td);
+      for (int e = 0; e < TS; ++e) ts += tile_time(seq[e]);
+      head = !big.empty() && TS > 0 && tb / big.size() >= 1.5 * ts / TS;
+      if (pack == 4) {
+        double flops = 0, bytes = 0;  // the call's algorithmic intensity
+        for (int i : order) {
+          const HostProblem& p = probs[i];
+          flops += 2.0 * p.M * p.N * p.K;
+          bytes += ((double)p.M * p.K * p.a_bits + (double)p.N * p.K * p.w_bits) / 8 + 2.0 * p.M * p.N;
+        }
+        head = head || (bytes > 0 && flops / bytes < kPackHeadFlopPerByte);
+      }
+    }
+    // XCD x's region tiles: first its own rectangle (region_tiles[x], in band order) up to cnt[x]; the
+    // rectangles' surplus tails then fill the XCDs that take more than their own (a piece stays one
+    // rectangle plus at most a band's worth of a neighbour: the panel reuse the rectangles bought)
+    std::vector<size_t> rb(9, 0);
+    for (int x = 0; x < 8; ++x) rb[x + 1] = rb[x] + region_tiles[x].size();
+    std::vector<std::vector<int>> pieces(8);
+    auto assign_pieces = [&]() {
+      std::vector<int> pool;
+      for (int x = 0; x < 8; ++x) {
+        pieces[x].clear();
+        const size_t own = rb[x + 1] - rb[x], take = std::min(own, (size_t)cnt[x]);
+        for (size_t k = 0; k < own; ++k) (k < take ? pieces[x] : pool).push_back((int)(rb[x] + k));
+      }
+      size_t p = 0;
+      for (int x = 0; x < 8; ++x)
+        while ((int)pieces[x].size() < cnt[x] && p < pool.size()) pieces[x].push_back(pool[p++]);
+    };
+    auto build_q = [&](int x, std::vector<int>* q) {
       q->clear();
       std::vector<int> bq;
-      for (int k = 0; k < cnt[x]; ++k) bq.push_back(-1 - (int)(off + k));  // (big tiles: -1 - index)
-      if (pack == 1) *q = bq;
+      for (int k : pieces[x]) bq.push_back(-1 - k);  // (big tiles: -1 - index)
+      if (head) *q = bq;
       q->insert(q->end(), small_q[x].begin(), small_q[x].end());
-      if (pack != 1) q->insert(q->end(), bq.begin(), bq.end());
+      if (!head) q->insert(q->end(), bq.begin(), bq.end());
       const size_t n = q->size(), tail = std::min(n, (size_t)(2 * chunk));
       auto tt = [&](int e) { return e < 0 ? tile_time(big[-1 - e]) : tile_time(seq[e]); };
       std::stable_sort(q->end() - tail, q->end(), [&](int a, int b) { return tt(a) > tt(b); });
@@ -1092,11 +1149,10 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     std::vector<std::vector<int>> q(8);
     double fin[8];
     auto rebuild = [&]() {
-      size_t off = 0;
+      assign_pieces();
       for (int x = 0; x < 8; ++x) {
-        build_q(x, off, &q[x]);
+        build_q(x, &q[x]);
         fin[x] = finish_of(q[x]);
-        off += cnt[x];
       }
     };
     rebuild();

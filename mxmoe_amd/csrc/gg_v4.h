@@ -73,6 +73,95 @@ __device__ __forceinline__ void v4_mma(const V4Frag<Cfg>& f, typename AccT<QT>::
 }
 
 template <class Cfg, int QT>
+__device__ __forceinline__ void v4_mma1(const V4Frag<Cfg>& f, int i, int j, typename AccT<QT>::type (&acc)[Cfg::FM][Cfg::FN]) {
+  if constexpr (QT == QT_I8) {
+    acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.b[j], f.a[i], acc[i][j], 0, 0, 0);
+  } else {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, f.b[j]), __builtin_bit_cast(v8h, f.a[i]),
+                                                       acc[i][j], 0, 0, 0);
+  }
+}
+
+// Epilogue of the v4d tile: epilogue_v3's arithmetic and staging, with the tile's row / column
+// scales read from the LDS stash (`sl`: SA of rows m0.. at [0, 256), SB of columns n0.. at [256, 512),
+// clamped at load time) instead of global loads at the epilogue's start (their L2 / HBM latency was
+// exposed at every tile boundary).
+template <class Cfg, int QT>
+__device__ __forceinline__ void epilogue_v4(const GGMeta& mt, typename AccT<QT>::type (&acc)[Cfg::FM][Cfg::FN],
+                                            const _Float16* sl, _Float16* __restrict__ C, int m0, int n0, uint8_t* lds) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N;
+  constexpr int RB = Cfg::WTN * 2, CPR = RB / 16;  // staged row bytes, 16-B chunks per row
+  uint8_t* reg = lds + wave * (Cfg::WTM * Cfg::WTN * 2);
+  const int mrow0 = m0 + wm * Cfg::WTM, ncol0 = n0 + wn * Cfg::WTN;
+  uint2 sbw[FN];
+  if constexpr (QT != QT_F16) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) sbw[j] = *reinterpret_cast<const uint2*>(sl + 256 + wn * Cfg::WTN + j * 16 + 4 * g);
+  }
+  auto pack_frag = [&](int i, int j, _Float16 sai) {
+    if constexpr (QT == QT_F16) return pack4_f16(acc[i][j]);
+    else return scale_pack4<0>(acc[i][j], sai, sbw[j]);
+  };
+  if ((mt.reserved2 & META_SILU) != 0) {  // fused SiLU (as gg_tile_v2): rows of WTN / 2 outputs
+    constexpr int ORB = Cfg::WTN, OCPR = ORB / 16;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = i * 16 + r16;
+      _Float16 sai = 0;
+      if constexpr (QT != QT_F16) sai = sl[wm * Cfg::WTM + ml];
+#pragma unroll
+      for (int jp = 0; jp < FN / 2; ++jp) {
+        const uint2 h = silu_mul4(pack_frag(i, 2 * jp, sai), pack_frag(i, 2 * jp + 1, sai));
+        const int q = 2 * jp + (g >> 1);
+        *reinterpret_cast<uint2*>(reg + ml * ORB + ((q ^ (ml & (OCPR - 1))) << 4) + (g & 1) * 8) = h;
+      }
+    }
+    constexpr int ORPI = 64 / OCPR;
+    const int ocol0 = ncol0 / 2, NO = N / 2;
+    _Float16* const obase = C + (int64_t)mrow0 * mt.ldc + ocol0;
+    const bool onarrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;
+#pragma unroll 4
+    for (int it = 0; it < Cfg::WTM / ORPI; ++it) {
+      const int row = it * ORPI + lane / OCPR, q = lane % OCPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(reg + row * ORB + ((q ^ (row & (OCPR - 1))) << 4));
+      if (mrow0 + row < M && ocol0 + q * 8 < NO) store_c16(obase, (int64_t)row * mt.ldc + q * 8, onarrow, v);
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = i * 16 + r16;
+    _Float16 sai = 0;
+    if constexpr (QT != QT_F16) sai = sl[wm * Cfg::WTM + ml];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const uint2 pk = pack_frag(i, j, sai);
+      const int q = 2 * j + (g >> 1);
+      *reinterpret_cast<uint2*>(reg + ml * RB + ((q ^ (ml & (CPR - 1))) << 4) + (g & 1) * 8) = pk;
+    }
+  }
+  constexpr int RPI = 64 / CPR;  // staged rows per wave-instruction
+  _Float16* const cbase = C + (int64_t)mrow0 * mt.ldc + ncol0;  // wave-uniform
+  const bool narrow = (int64_t)Cfg::WTM * mt.ldc < (int64_t)1 << 29;
+#pragma unroll 4
+  for (int it = 0; it < Cfg::WTM / RPI; ++it) {
+    const int row = it * RPI + lane / CPR, q = lane % CPR;
+    const uint4 v = *reinterpret_cast<const uint4*>(reg + row * RB + ((q ^ (row & (CPR - 1))) << 4));
+    const int m = mrow0 + row, n = ncol0 + q * 8;
+    if (m < M && n < N) store_c16(cbase, (int64_t)row * mt.ldc + q * 8, narrow, v);
+  }
+}
+
+// OPT & 1: in-kernel s_memtime stamps of the steady stages (diagnostics build: per wave the cycles of
+// segments 1 / 2 / 3, the stage-end vmcnt wait and the barrier, summed over the steady stages, into
+// g_gg_stamp — slot (block, wave): {seg1, seg2, seg3, stages}, slot (block, wave + 4): {vm, bar, 0,
+// stages}; tools/stamps_v4.py)
+template <class Cfg, int QT, int OPT = 0>
 __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __restrict__ A,
                                            const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
                                            const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0, int n0,
@@ -134,6 +223,15 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+  // int paths: this thread's row and column scale (one register across the mainloop), stashed in the
+  // dead ring after it (past the 128-KiB epilogue image) for epilogue_v4
+  constexpr int STASH = 128 * 1024;
+  uint32_t sc_t = 0;  // SA | SB << 16
+  if constexpr (qt_scaled(QT)) {
+    const uint16_t a = __builtin_bit_cast(uint16_t, SA[min(m0 + min(tid, Cfg::BM - 1), M - 1)]);
+    const uint16_t b = __builtin_bit_cast(uint16_t, SB[min(n0 + tid, N - 1)]);
+    sc_t = (uint32_t)a | ((uint32_t)b << 16);
+  }
 
   const int swz = (r16 >> 1) & 7;
   const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u, b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
@@ -166,57 +264,89 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
     int s = 1;
     // steady state: A(s+1) and B(s+2) exist and are full stages; one basic block per stage
     const int nsteady = nst_full - 2;
+    // steady state, hand-chunked (OPT & 1, the default build): every chunk is fenced by
+    // sched_barrier(0), so the interleave of reads, MFMAs and DMA pieces is fixed in program order
+    // (left to sched_group_barrier, hipcc bunched the int8 body's B pieces and F1 reads at the end of
+    // the second segment: the reads' latency and 8 back-to-back DMA issues exposed before the barrier)
+    //   seg 1 (C1 = 8 chunks):  2 reads of F0 (B fragments first, then A) | S1 / C1 MFMAs of F1's deferred
+    //                          rows | 1 A piece per C1 / GA chunks
+    //   seg 2 (C2 = 16 chunks): 1 read of F1 (B, then the A rows seg 3 needs, then the rest) | S2 / C2
+    //                          MFMAs of F0, row-major | 1 B piece per C2 / GB chunks
+    //   seg 3: F1 rows 0..H, then the stage-end wait and barrier
+    constexpr int NR = FM + FN, S1 = H * FN, S2 = FM * FN, C1 = 8, C2 = 16;
+    static_assert(S1 % C1 == 0 && S2 % C2 == 0 && C1 % GA == 0 && C2 % GB == 0, "v4d chunking");
+    const uint8_t* const a0 = ringA + a_row;
+    const uint8_t* const b0 = ringB + b_row;
+    uint64_t st_seg[3] = {0, 0, 0}, st_vm = 0, st_bar = 0;
     for (; s < nsteady; ++s) {
-      // three segments fenced by sched_barrier (MFMAs would otherwise drift across the stage-end
-      // barrier, which orders memory only): inside each, sched_group_barrier fixes the interleave
-      constexpr int NR = FM + FN, S1 = H * FN, S2 = FM * FN;
-      // (1) F0's reads two per MFMA of F1's deferred rows, the A pieces spread over the rest of them
-      rd(F0, s, off0);
-      v4_mma<Cfg, QT, H, FM>(F1, acc);
-      dma_a(s + 1, true);
-      {
-        constexpr int R1 = (NR + 1) / 2 < S1 ? (NR + 1) / 2 : S1;
-        constexpr int K1 = (S1 - R1) / GA, K1R = S1 - R1 - K1 * GA;
+      [[maybe_unused]] uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+      if constexpr ((OPT & 1) != 0) t0 = __builtin_amdgcn_s_memtime();
+      const uint8_t* As = a0 + (s & 1) * Cfg::SLOT;
+      const uint8_t* Bs = b0 + (s % 3) * Cfg::SLOT;
+      auto rd1 = [&](Frag& f, int k, uint32_t off) {  // read k: B fragments 0..FN-1, then A 0..FM-1
+        if (k < FN) f.b[k] = *reinterpret_cast<const v4i*>(Bs + k * 2048 + off);
+        else f.a[k - FN] = *reinterpret_cast<const v4i*>(As + (k - FN) * 2048 + off);
+      };
+      const int kb_a = (ks0 + s + 1) * Cfg::BKB, kb_b = (ks0 + s + 2) * Cfg::BKB;
+      uint8_t* const da = ringA + ((s + 1) & 1) * Cfg::SLOT + wave * GA * 1024;
+      uint8_t* const db = ringB + ((s + 2) % 3) * Cfg::SLOT + wave * GB * 1024;
 #pragma unroll
-        for (int q = 0; q < R1; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        }
+      for (int c = 0; c < C1; ++c) {
 #pragma unroll
-        for (int q = 0; q < GA; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, K1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        for (int r = 0; r < (NR + C1 - 1) / C1; ++r)
+          if (c * ((NR + C1 - 1) / C1) + r < NR) rd1(F0, c * ((NR + C1 - 1) / C1) + r, off0);
+#pragma unroll
+        for (int x = 0; x < S1 / C1; ++x) {
+          const int idx = c * (S1 / C1) + x, i = H + idx / FN, j = idx % FN;
+          v4_mma1<Cfg, QT>(F1, i, j, acc);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, K1R, 0);
+        if (c % (C1 / GA) == 0) bdma16(rsA, da + (c / (C1 / GA)) * 1024, voA[c / (C1 / GA)], kb_a);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      // (2) F0's MFMAs with F1's reads early (one per 2 MFMAs) and the B pieces spread over the rest
-      v4_mma<Cfg, QT, 0, FM>(F0, acc);
-      rd(F1, s, off1);
-      dma_b(s + 2, true);
-      {
-        constexpr int R2 = 2 * NR < S2 ? NR : S2 / 2;
-        constexpr int K2 = (S2 - 2 * R2) / GB, K2R = S2 - 2 * R2 - K2 * GB;
+      if constexpr ((OPT & 1) != 0) t1 = __builtin_amdgcn_s_memtime();
 #pragma unroll
-        for (int q = 0; q < R2; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, NR - R2, 0);
+      for (int c = 0; c < C2; ++c) {
+        if (c < NR) rd1(F1, c, off1);
 #pragma unroll
-        for (int q = 0; q < GB; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, K2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        for (int x = 0; x < S2 / C2; ++x) {
+          const int idx = c * (S2 / C2) + x, i = idx / FN, j = idx % FN;
+          v4_mma1<Cfg, QT>(F0, i, j, acc);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, K2R, 0);
+        if (c % (C2 / GB) == 0) bdma16(rsB, db + (c / (C2 / GB)) * 1024, voB[c / (C2 / GB)], kb_b);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      // (3) F1 rows 0..H, then the stage-end wait and barrier
+      if constexpr ((OPT & 1) != 0) t2 = __builtin_amdgcn_s_memtime();
       v4_mma<Cfg, QT, 0, H>(F1, acc);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((OPT & 1) != 0) t3 = __builtin_amdgcn_s_memtime();
       wait_vmcnt<GB>();
+      if constexpr ((OPT & 1) != 0) t4 = __builtin_amdgcn_s_memtime();
       lds_barrier();  // B(s)
+      if constexpr ((OPT & 1) != 0) {
+        const uint64_t t5 = __builtin_amdgcn_s_memtime();
+        st_seg[0] += t1 - t0;
+        st_seg[1] += t2 - t1;
+        st_seg[2] += t3 - t2;
+        st_vm += t4 - t3;
+        st_bar += t5 - t4;
+      }
     }
+#ifdef MXMOE_LAB
+    if constexpr ((OPT & 1) != 0) {
+      if (lane == 0 && blockIdx.x < kStampBlocks && nsteady > 1) {
+        uint64_t* o = g_gg_stamp + ((size_t)blockIdx.x * 8 + wave) * 4;
+        o[0] = st_seg[0];
+        o[1] = st_seg[1];
+        o[2] = st_seg[2];
+        o[3] = (uint64_t)(nsteady - 1);
+        uint64_t* o2 = g_gg_stamp + ((size_t)blockIdx.x * 8 + wave + 4) * 4;
+        o2[0] = st_vm;
+        o2[1] = st_bar;
+        o2[2] = 0;
+        o2[3] = (uint64_t)(nsteady - 1);
+      }
+    }
+#endif
     for (; s < nst; ++s) {  // the last stages (K tail, no more pieces to issue)
       rd(F0, s, off0);
       v4_mma<Cfg, QT, H, FM>(F1, acc);
@@ -233,11 +363,17 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
   } else {
     __syncthreads();
   }
+  _Float16* const sl = reinterpret_cast<_Float16*>(lds + STASH);
+  if constexpr (qt_scaled(QT)) {
+    reinterpret_cast<uint16_t*>(sl)[tid] = (uint16_t)sc_t;  // (the ring is drained: every wave passed the
+    reinterpret_cast<uint16_t*>(sl)[256 + tid] = (uint16_t)(sc_t >> 16);  // last stage's barrier)
+  }
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
-  epilogue_v3<Cfg, QT>(mt, acc, SA, SB, C, m0, n0, lds);
+  if constexpr (qt_scaled(QT)) __syncthreads();        // the stash is visible to every wave
+  epilogue_v4<Cfg, QT>(mt, acc, sl, C, m0, n0, lds);
 }
 
-template <int QM>
+template <int QM, int OPT = 0>
 __global__ __launch_bounds__(256, 1) void gg_v4_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[V4Cfg<256>::LDS_BYTES];
   const TileDesc td = args.tiles[blockIdx.x];
@@ -259,12 +395,12 @@ __global__ __launch_bounds__(256, 1) void gg_v4_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
-    if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
-    else gg_tile_v4<V4Cfg<128>, QT_I8>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v4<V4Cfg<128>, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
-    if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
-    else if (cls == 1) gg_tile_v4<V4Cfg<128>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
-    else gg_tile_v4<V4Cfg<64>, QT_F16>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else if (cls == 1) gg_tile_v4<V4Cfg<128>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v4<V4Cfg<64>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   }
 }
 

@@ -18,7 +18,7 @@ for cfg in "$@"; do
   done
 done
 python3 - "$OUT" "$@" <<'PY'
-import csv, glob, json, sys
+import csv, glob, json, os, sys
 out, cfgs = sys.argv[1], sys.argv[2:]
 res = {}
 for cfg in cfgs:
@@ -33,6 +33,7 @@ for cfg in cfgs:
         d[gg] = {"fetch_bytes_x2": 2 * v["FETCH_SIZE"] * 1024, "write_bytes": v["WRITE_SIZE"] * 1024,
                  "hbm_bytes": kb * 1024}
     d["hbm_bytes_per_step"] = d["gate_up"]["hbm_bytes"] + d["down"]["hbm_bytes"]
+    d["_round"] = os.environ.get("PMC_ROUND", "untagged")  # which round's tree measured it (bench.py emits it)
     res[cfg] = d
 res["_method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes over tools/kbench.py (AUTO variant), "
                   "mean per dispatch, KB -> bytes, FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md §HBM)")
