@@ -389,15 +389,21 @@ void launch_v4(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   switch (qmask & 511) {
     case 1: launch_v4_q<1, OPT>(a, grid, s); break;
     case 2: launch_v4_q<2, OPT>(a, grid, s); break;
+    case 4: launch_v4_q<4, OPT>(a, grid, s); break;
+#ifndef MXMOE_LAB_FAST
+    case 6: launch_v4_q<6, OPT>(a, grid, s); break;
+    default: launch_v4_q<7, OPT>(a, grid, s); break;
+#else
     default: launch_v4_q<3, OPT>(a, grid, s); break;
+#endif
   }
 }
 template <int OPT = 0>
 Variant make_v4(const char* name) {
   Variant v = v2_base(name, V4Cfg<256>::LDS_BYTES);
   for (int q = 0; q < QT_COUNT; ++q)
-    if (q != QT_F16 && q != QT_I8) v.geom[q] = {0, 0, 0, 0};
-  v.geom[QT_F16].threads = v.geom[QT_I8].threads = 256;
+    if (q != QT_F16 && q != QT_I8 && q != QT_I4) v.geom[q] = {0, 0, 0, 0};
+  v.geom[QT_F16].threads = v.geom[QT_I8].threads = v.geom[QT_I4].threads = 256;
   v.threads = 256;
   v.launch = &launch_v4<OPT>;
   return v;
@@ -459,6 +465,7 @@ const std::vector<Variant>& variants() {
       make_v2<kV2x>("x_v2x"),
       make_v4("x_v4d_256x256_w4_1wave"),
       make_v4<1>("abl_v4d_stamp"),
+      make_v3<128, 2, 3, 2>("v3_256x128_w4_dma_ring3_2wg"),  // the w4a4 AUTO kernel (A/B reference)
       make_v2<kV2x | V2_I4NOPAIR>("x_v2x_i4nopair"),
       make_v2<kV2x | V2_PLAINST>("x_v2x_plainst"),
       make_v2<kV2x | V2_TRACE>("abl_v2x_trace"),

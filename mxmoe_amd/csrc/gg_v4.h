@@ -82,6 +82,35 @@ __device__ __forceinline__ void v4_mma1(const V4Frag<Cfg>& f, int i, int j, type
   }
 }
 
+// int4 (w4a4): a 16-B fragment read holds 32 codes of one 64-B K half = two MFMA K steps (t = 0: words
+// 0-1, t = 1: words 2-3, the same K map for A and B, as gg_tile_v3); each step's operands are the
+// nibbles widened to 16 * q int8 (widen_i4: the int32 sum is exactly 256 * sum(a * b))
+template <class Cfg>
+struct V4Wide {
+  v4i b[Cfg::FN];  // B fragments of one K step, widened
+};
+__device__ __forceinline__ v4i v4_widen(const v4i& raw, int t) { return widen_i4(v2i{raw[2 * t], raw[2 * t + 1]}); }
+template <class Cfg>
+__device__ __forceinline__ void v4_widen_b(const V4Frag<Cfg>& f, int t, V4Wide<Cfg>& w) {
+#pragma unroll
+  for (int j = 0; j < Cfg::FN; ++j) w.b[j] = v4_widen(f.b[j], t);
+}
+// one int4 K step of fragment row i (A widened here), all columns
+template <class Cfg>
+__device__ __forceinline__ void v4_mma_i4row(const V4Frag<Cfg>& f, const V4Wide<Cfg>& w, int t, int i,
+                                             v4i (&acc)[Cfg::FM][Cfg::FN]) {
+  const v4i aw = v4_widen(f.a[i], t);
+#pragma unroll
+  for (int j = 0; j < Cfg::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(w.b[j], aw, acc[i][j], 0, 0, 0);
+}
+template <class Cfg>
+__device__ __forceinline__ void v4_mma_i4(const V4Frag<Cfg>& f, int t, v4i (&acc)[Cfg::FM][Cfg::FN]) {
+  V4Wide<Cfg> w;
+  v4_widen_b<Cfg>(f, t, w);
+#pragma unroll
+  for (int i = 0; i < Cfg::FM; ++i) v4_mma_i4row<Cfg>(f, w, t, i, acc);
+}
+
 // Epilogue of the v4d tile: epilogue_v3's arithmetic and staging, with the tile's row / column
 // scales read from the LDS stash (`sl`: SA of rows m0.. at [0, 256), SB of columns n0.. at [256, 512),
 // clamped at load time) instead of global loads at the epilogue's start (their L2 / HBM latency was
@@ -105,7 +134,7 @@ __device__ __forceinline__ void epilogue_v4(const GGMeta& mt, typename AccT<QT>:
   }
   auto pack_frag = [&](int i, int j, _Float16 sai) {
     if constexpr (QT == QT_F16) return pack4_f16(acc[i][j]);
-    else return scale_pack4<0>(acc[i][j], sai, sbw[j]);
+    else return scale_pack4<(QT == QT_I4) ? 8 : 0>(acc[i][j], sai, sbw[j]);
   };
   if ((mt.reserved2 & META_SILU) != 0) {  // fused SiLU (as gg_tile_v2): rows of WTN / 2 outputs
     constexpr int ORB = Cfg::WTN, OCPR = ORB / 16;
@@ -240,6 +269,26 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
     v4_read<Cfg>(f, ringA + (t & 1) * Cfg::SLOT + a_row, ringB + (t % 3) * Cfg::SLOT + b_row, off);
   };
 
+  // the three MFMA parts of a stage (int8 / fp16: all rows of half 0, then rows 0..H of half 1 before
+  // the stage-end barrier and rows H..FM after it; int4: both K steps of half 0, then step 0 of half 1
+  // before the barrier and step 1 after it)
+  auto mma_all = [&](const Frag& f) {
+    if constexpr (QT == QT_I4) {
+      v4_mma_i4<Cfg>(f, 0, acc);
+      v4_mma_i4<Cfg>(f, 1, acc);
+    } else {
+      v4_mma<Cfg, QT, 0, FM>(f, acc);
+    }
+  };
+  auto mma_first = [&](const Frag& f) {
+    if constexpr (QT == QT_I4) v4_mma_i4<Cfg>(f, 0, acc);
+    else v4_mma<Cfg, QT, 0, H>(f, acc);
+  };
+  auto mma_second = [&](const Frag& f) {
+    if constexpr (QT == QT_I4) v4_mma_i4<Cfg>(f, 1, acc);
+    else v4_mma<Cfg, QT, H, FM>(f, acc);
+  };
+
   if (nst > 0) {
     Frag F0, F1;
     dma_a(0, full(0));
@@ -254,10 +303,10 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
     // iteration 0 (no deferred rows yet)
     rd(F0, 0, off0);
     if (nst > 1) dma_a(1, full(1));
-    v4_mma<Cfg, QT, 0, FM>(F0, acc);
+    mma_all(F0);
     rd(F1, 0, off1);
     if (nst > 2) dma_b(2, full(2));
-    v4_mma<Cfg, QT, 0, H>(F1, acc);
+    mma_first(F1);
     if (nst > 2) wait_vmcnt<GB>();
     else wait_vmcnt<0>();
     lds_barrier();  // B(0)
@@ -278,6 +327,67 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
     const uint8_t* const a0 = ringA + a_row;
     const uint8_t* const b0 = ringB + b_row;
     uint64_t st_seg[3] = {0, 0, 0}, st_vm = 0, st_bar = 0;
+    if constexpr (QT == QT_I4) {
+      // int4 steady stage: 256 MFMAs (4 K steps x 64) and 384 widening VALU per wave, hand-chunked so
+      // every widened B set is built a chunk row ahead of its first MFMA:
+      //   seg 1 (8 chunks, one fragment row each): F1 step 1 (A widened per row, B set wb1 built in
+      //          seg 3) | F0's 16 reads, 2 per chunk | F0's B step 0 widened in chunks 4-7 | A pieces
+      //   seg 2 (16 chunks: step 0 rows, then step 1 rows of F0) | F1's 16 reads, 1 per chunk | F0's B
+      //          step 1 widened in chunks 0-7, F1's B step 0 in chunks 8-15 | B pieces
+      //   seg 3 (8 chunks): F1 step 0 | F1's B step 1 widened, 1 per chunk; then wait + barrier
+      // (written for the 256-row tile; the 128-row class runs every stage through the plain loop below)
+      if constexpr (FM == 8 && FN == 8 && GA == 8 && GB == 8) {
+      // one widened B set live at a time (register pressure: the pre-widened variant kept 2-3 sets and
+      // hipcc shuffled accumulators through the AGPRs, 340 v_accvgpr moves per stage): each K-step
+      // block widens its 8 B fragments at its start, then row by row (A widened per row, 8 MFMAs)
+      V4Wide<Cfg> w;
+      for (; s < nsteady; ++s) {
+        const uint8_t* As = a0 + (s & 1) * Cfg::SLOT;
+        const uint8_t* Bs = b0 + (s % 3) * Cfg::SLOT;
+        auto rd1 = [&](Frag& f, int k, uint32_t off) {
+          if (k < FN) f.b[k] = *reinterpret_cast<const v4i*>(Bs + k * 2048 + off);
+          else f.a[k - FN] = *reinterpret_cast<const v4i*>(As + (k - FN) * 2048 + off);
+        };
+        const int kb_a = (ks0 + s + 1) * Cfg::BKB, kb_b = (ks0 + s + 2) * Cfg::BKB;
+        uint8_t* const da = ringA + ((s + 1) & 1) * Cfg::SLOT + wave * GA * 1024;
+        uint8_t* const db = ringB + ((s + 2) % 3) * Cfg::SLOT + wave * GB * 1024;
+        // seg 1: F1 step 1 (the deferred block) | F0's 16 reads | A pieces
+        v4_widen_b<Cfg>(F1, 1, w);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          rd1(F0, 2 * c, off0);
+          rd1(F0, 2 * c + 1, off0);
+          v4_mma_i4row<Cfg>(F1, w, 1, c, acc);
+          bdma16(rsA, da + c * 1024, voA[c], kb_a);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // seg 2: F0 steps 0 and 1 | F1's 16 reads | B pieces
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          v4_widen_b<Cfg>(F0, t, w);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            rd1(F1, 8 * t + c, off1);
+            v4_mma_i4row<Cfg>(F0, w, t, c, acc);
+            if ((c & 1) == 0) bdma16(rsB, db + (4 * t + (c >> 1)) * 1024, voB[4 * t + (c >> 1)], kb_b);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        // seg 3: F1 step 0
+        v4_widen_b<Cfg>(F1, 0, w);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          v4_mma_i4row<Cfg>(F1, w, 0, c, acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        wait_vmcnt<GB>();
+        lds_barrier();  // B(s)
+      }
+      }
+    } else
     for (; s < nsteady; ++s) {
       [[maybe_unused]] uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
       if constexpr ((OPT & 1) != 0) t0 = __builtin_amdgcn_s_memtime();
@@ -349,17 +459,17 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
 #endif
     for (; s < nst; ++s) {  // the last stages (K tail, no more pieces to issue)
       rd(F0, s, off0);
-      v4_mma<Cfg, QT, H, FM>(F1, acc);
+      mma_second(F1);
       if (s + 1 < nst) dma_a(s + 1, full(s + 1));
-      v4_mma<Cfg, QT, 0, FM>(F0, acc);
+      mma_all(F0);
       rd(F1, s, off1);
       if (s + 2 < nst) dma_b(s + 2, full(s + 2));
-      v4_mma<Cfg, QT, 0, H>(F1, acc);
+      mma_first(F1);
       if (s + 2 < nst) wait_vmcnt<GB>();
       else wait_vmcnt<0>();
       lds_barrier();  // B(s)
     }
-    v4_mma<Cfg, QT, H, FM>(F1, acc);  // the deferred rows of the last stage
+    mma_second(F1);  // the deferred part of the last stage
   } else {
     __syncthreads();
   }
@@ -397,6 +507,9 @@ __global__ __launch_bounds__(256, 1) void gg_v4_kernel(GGArgs args) {
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v4<V4Cfg<128>, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+  } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
+    if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_I4, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v4<V4Cfg<128>, QT_I4, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_v4<V4Cfg<128>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
