@@ -5,6 +5,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export PMC_ROUND="round 6"
+mkdir -p gpurun_out/r06/traffic
 PMC_OUT=gpurun_out/r06/traffic/b8192 timeout -k 10 900 bash tools/pmc_traffic.sh fp16 w8a8 w4a4 mixed ds2_mixed > gpurun_out/r06/traffic_b8192.log 2>&1 || { tail -20 gpurun_out/r06/traffic_b8192.log; exit 1; }
 PMC_OUT=gpurun_out/r06/traffic/b512 KB_ARGS="--bs 512" timeout -k 10 300 bash tools/pmc_traffic.sh w4a16_w8a8 > gpurun_out/r06/traffic_b512.log 2>&1 || { tail -20 gpurun_out/r06/traffic_b512.log; exit 1; }
 python3 - <<'PY'
