@@ -574,9 +574,6 @@ constexpr double kWoSmallMeanRows = 512.0;
 constexpr double kSmallMeanRows = 80.0;
 constexpr double kSmallMeanRowsI4 = 112.0;
 constexpr double kSplitCUs = 256.0;  // MI355X compute units: the planner's notion of "one CU's share"
-// XCD packing (plan_host): region tiles at the queue head for calls below this many flops per
-// algorithmic byte (qwen2_moe layer 11: fp16 524-593, w8a8 849-919, mixed 987-1193, w4a4 1233-1268)
-constexpr double kPackHeadFlopPerByte = 700.0;
 
 int variant_index(const char* name) {
   for (size_t i = 0; i < variants().size(); ++i)
@@ -953,6 +950,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     return out->gm != 0;
   };
   int groups = 0, n_region = 0;
+  bool region_a16 = false;
   std::vector<TileDesc> seq;                // chunked tiles
   std::vector<int> seq_end;                 // per seq tile: end of its problem's run in seq
   std::vector<std::vector<TileDesc>> region_tiles(8);  // per XCD
@@ -965,6 +963,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
     Region rg;
     if (region_of(order[row], &rg)) {
       ++n_region;
+      region_a16 = region_a16 || probs[order[row]].a_bits == 16;
       for (int x = 0; x < 8; ++x) {
         const int mb0 = (x / rg.gn) * rg.r, mb1 = std::min((int)mt.size(), mb0 + rg.r);
         const int nb0 = (x % rg.gn) * rg.c, nb1 = std::min(nt, nb0 + rg.c);
@@ -1057,10 +1056,11 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
   // pieces (XCD x's piece overlaps its rectangle, so the panel reuse of the rectangles is kept).
   // Default (pack 4, product): packing for the MoE call shape — ONE region problem (the shared expert)
   // beside >= 8 whole small problems — with the region tiles at the queue head when they are the long
-  // ones (down: K 4x the routed K; LPT) or when the call streams many bytes per flop (arithmetic
-  // intensity under kPackHeadFlopPerByte: the 16-bit calls, whose head placement cut the fp16 gate_up
-  // counter bytes 2.97 -> 2.35 GB and ran 2.4 % faster, where w8a8 gate_up at the head ran 4 % slower
-  // (profiles/r06/pack/)); every other call keeps the chunked placement below. Lab A/B:
+  // ones (down: K 4x the routed K; LPT) or when the region problem's A is 16-bit (its panels stream
+  // twice the bytes per flop: the fp16 gate_up call's head placement cut its counter bytes 2.97 ->
+  // 2.35 GB and ran 2.4 % faster, where w8a8 gate_up at the head ran 4 % slower, profiles/r06/pack/;
+  // an arithmetic-intensity cut in its place also sent the int calls of small batches to the head,
+  // 3-8 % slower at bs 2048, profiles/r06/plan3/); every other call keeps the chunked placement. Lab A/B:
   // MXMOE_GG_XCD_PACK = 0 off, 1 always head, 2 always tail, 3 head only for long region tiles.
   const char* pack_env = planner_knob("MXMOE_GG_XCD_PACK");
   const int pack = pack_env ? atoi(pack_env) : 4;
@@ -1107,15 +1107,7 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       for (const TileDesc& td : big) tb += tile_time(td);
       for (int e = 0; e < TS; ++e) ts += tile_time(seq[e]);
       head = !big.empty() && TS > 0 && tb / big.size() >= 1.5 * ts / TS;
-      if (pack == 4) {
-        double flops = 0, bytes = 0;  // the call's algorithmic intensity
-        for (int i : order) {
-          const HostProblem& p = probs[i];
-          flops += 2.0 * p.M * p.N * p.K;
-          bytes += ((double)p.M * p.K * p.a_bits + (double)p.N * p.K * p.w_bits) / 8 + 2.0 * p.M * p.N;
-        }
-        head = head || (bytes > 0 && flops / bytes < kPackHeadFlopPerByte);
-      }
+      if (pack == 4) head = head || region_a16;  // a 16-bit region problem (fp16 / bf16 / weight-only A)
     }
     // XCD x's region tiles: first its own rectangle (region_tiles[x], in band order) up to cnt[x]; the
     // rectangles' surplus tails then fill the XCDs that take more than their own (a piece stays one

@@ -483,6 +483,159 @@ __device__ __forceinline__ void gg_tile_v4(const GGMeta& mt, const uint8_t* __re
   epilogue_v4<Cfg, QT>(mt, acc, sl, C, m0, n0, lds);
 }
 
+// v4d's int4 (w4a4) tile, ONE fragment set (the int4 body of gg_tile_v4 kept two sets plus widened
+// operands and hipcc spilled its steady loop into the AGPRs). A 64-B K half of a fragment holds two
+// MFMA K steps (t = 0, 1; V4Wide / v4_widen as above). Per K half: step 0 — widen the 8 B fragments,
+// then row by row widen A and run 8 MFMAs; step 1 — widen B again (words 2-3), and as each raw
+// fragment is consumed the NEXT half's read goes into its registers (B reads at the step's start, the
+// A read of row i after row i's MFMAs), so the reads of the next half run under this step's 64 MFMAs.
+// One barrier per stage, between the second half's two steps: every wave has consumed all its reads of
+// stage s there (the step-0 widening waited for them), and stage s+1 must have landed before the
+// step-1 reads of its first half. LDS-DMA (v2x's image and buffer form, as gg_tile_v4): B(s+2) one
+// piece per row of stage s's first step (its slot last held stage s-1, free since B(s-1)); A(s+2)
+// one per row of the post-barrier step (its slot held stage s). At B(s): vmcnt(GB) leaves B(s+2) in
+// flight; A(s+1) was issued a whole stage (4096 MFMA cycles) before.
+template <class Cfg, int OPT = 0>
+__device__ __forceinline__ void gg_tile_v4_i4(const GGMeta& mt, const uint8_t* __restrict__ A,
+                                              const uint8_t* __restrict__ B, const _Float16* __restrict__ SA,
+                                              const _Float16* __restrict__ SB, _Float16* __restrict__ C, int m0,
+                                              int n0, uint8_t* lds, const SplitK& sk) {
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, GA = Cfg::GA, GB = Cfg::GB;
+  static_assert(GA % FM == 0 || FM % GA == 0, "A pieces per row");
+  typedef V4Frag<Cfg> Frag;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WN, wn = wave % Cfg::WN;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int M = mt.M, N = mt.N, kbytes = mt.kbytes;
+  const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
+  const int nst = sk.nst, ks0 = sk.ks0;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(A) + (int64_t)m0 * lda, (short)0, (int)(min(M - m0, Cfg::BM) * lda), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(B) + (int64_t)n0 * ldb, (short)0, (int)(min(N - n0, Cfg::BN) * ldb), 0x00020000);
+  uint32_t voA[GA], voB[GB];
+  {
+    const int rsub = lane >> 3, p = lane & 7;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int row = (wave * GA + j) * 8 + rsub;
+      voA[j] = (uint32_t)(row * lda) + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int row = (wave * GB + j) * 8 + rsub;
+      voB[j] = (uint32_t)(row * ldb) + ((p ^ ((row >> 1) & 7)) << 4);
+    }
+  }
+  auto kc_of = [&](int G, int j) { return ((lane & 7) ^ ((((wave * G + j) * 8 + (lane >> 3)) >> 1) & 7)) << 4; };
+  uint8_t* const ringA = lds;
+  uint8_t* const ringB = lds + 2 * Cfg::SLOT;
+  const int nst_full = (ks0 + nst) * Cfg::BKB > kbytes ? nst - 1 : nst;
+  // piece j of operand A / B of stage t (`full`: no K-tail lanes)
+  auto pa = [&](int t, int j, bool full) {
+    const int kb = (ks0 + t) * Cfg::BKB;
+    bdma16(rsA, ringA + (t & 1) * Cfg::SLOT + (wave * GA + j) * 1024,
+           full || kb + kc_of(GA, j) < kbytes ? voA[j] : 0x80000000u, kb);
+  };
+  auto pb = [&](int t, int j, bool full) {
+    const int kb = (ks0 + t) * Cfg::BKB;
+    bdma16(rsB, ringB + (t % 3) * Cfg::SLOT + (wave * GB + j) * 1024,
+           full || kb + kc_of(GB, j) < kbytes ? voB[j] : 0x80000000u, kb);
+  };
+
+  v4i acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  constexpr int STASH = 128 * 1024;
+  uint32_t sc_t;
+  {
+    const uint16_t a = __builtin_bit_cast(uint16_t, SA[min(m0 + min(tid, Cfg::BM - 1), M - 1)]);
+    const uint16_t b = __builtin_bit_cast(uint16_t, SB[min(n0 + tid, N - 1)]);
+    sc_t = (uint32_t)a | ((uint32_t)b << 16);
+  }
+  const int swz = (r16 >> 1) & 7;
+  const uint32_t a_row = (uint32_t)(wm * Cfg::WTM + r16) * 128u, b_row = (uint32_t)(wn * Cfg::WTN + r16) * 128u;
+  const uint32_t offh[2] = {(uint32_t)((g ^ swz) << 4), (uint32_t)(((4 + g) ^ swz) << 4)};
+  auto a_src = [&](int t, int h, int i) { return ringA + (t & 1) * Cfg::SLOT + a_row + i * 2048 + offh[h]; };
+  auto b_src = [&](int t, int h, int j) { return ringB + (t % 3) * Cfg::SLOT + b_row + j * 2048 + offh[h]; };
+
+  if (nst > 0) {
+    Frag F;
+    V4Wide<Cfg> w;
+    pa(0, 0, nst_full > 0);
+    for (int j = 1; j < GA; ++j) pa(0, j, nst_full > 0);
+    for (int j = 0; j < GB; ++j) pb(0, j, nst_full > 0);
+    if (nst > 1) {
+      for (int j = 0; j < GB; ++j) pb(1, j, nst_full > 1);
+      wait_vmcnt<GB>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    lds_barrier();  // B(-1): stage 0 landed
+#pragma unroll
+    for (int j = 0; j < FN; ++j) F.b[j] = *reinterpret_cast<const v4i*>(b_src(0, 0, j));
+#pragma unroll
+    for (int i = 0; i < FM; ++i) F.a[i] = *reinterpret_cast<const v4i*>(a_src(0, 0, i));
+    if (nst > 1)
+      for (int j = 0; j < GA; ++j) pa(1, j, nst_full > 1);  // A(1): its slot is free (never used)
+    // one K step of the current half: B widened, then rows; `nx` (next half's reads) go into the
+    // registers each fragment frees: t = 1 only
+    auto step = [&](int t, bool reads, int rt, int rh, int dma, int ds) __attribute__((always_inline)) {
+      // dma: 0 none, 1 = B pieces of stage ds (one per row), 2 = A pieces of stage ds
+      v4_widen_b<Cfg>(F, t, w);
+      if (reads) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) F.b[j] = *reinterpret_cast<const v4i*>(b_src(rt, rh, j));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        v4_mma_i4row<Cfg>(F, w, t, i, acc);
+        if (reads) F.a[i] = *reinterpret_cast<const v4i*>(a_src(rt, rh, i));
+        if (dma == 1) {
+#pragma unroll
+          for (int q = i * GB / FM; q < (i + 1) * GB / FM; ++q) pb(ds, q, ds < nst_full);
+        } else if (dma == 2) {
+#pragma unroll
+          for (int q = i * GA / FM; q < (i + 1) * GA / FM; ++q) pa(ds, q, ds < nst_full);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    int s = 0;
+    const int nsteady = nst - 2;  // stages whose B(s+2) / A(s+2) exist (the K tail: `full` per stage)
+    for (; s < nsteady; ++s) {
+      step(0, false, 0, 0, 1, s + 2);  // half 0, step 0 | B(s+2)
+      step(1, true, s, 1, 0, 0);       // half 0, step 1 | reads of half 1
+      step(0, false, 0, 0, 0, 0);      // half 1, step 0
+      wait_vmcnt<GB>();
+      lds_barrier();                   // B(s)
+      step(1, true, s + 1, 0, 2, s + 2);  // half 1, step 1 | reads of stage s+1 half 0 | A(s+2)
+    }
+    for (; s < nst; ++s) {  // the last two stages (no more pieces)
+      step(0, false, 0, 0, 0, 0);
+      step(1, true, s, 1, 0, 0);
+      step(0, false, 0, 0, 0, 0);
+      wait_vmcnt<0>();
+      lds_barrier();
+      if (s + 1 < nst) step(1, true, s + 1, 0, 0, 0);
+      else step(1, false, 0, 0, 0, 0);
+    }
+  } else {
+    __syncthreads();
+  }
+  _Float16* const sl = reinterpret_cast<_Float16*>(lds + STASH);
+  reinterpret_cast<uint16_t*>(sl)[tid] = (uint16_t)sc_t;
+  reinterpret_cast<uint16_t*>(sl)[256 + tid] = (uint16_t)(sc_t >> 16);
+  if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;
+  __syncthreads();
+  epilogue_v4<Cfg, QT_I4>(mt, acc, sl, C, m0, n0, lds);
+}
+
 template <int QM, int OPT = 0>
 __global__ __launch_bounds__(256, 1) void gg_v4_kernel(GGArgs args) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[V4Cfg<256>::LDS_BYTES];
@@ -508,8 +661,8 @@ __global__ __launch_bounds__(256, 1) void gg_v4_kernel(GGArgs args) {
     if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else gg_tile_v4<V4Cfg<128>, QT_I8, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_I4)) && mt.qtype == QT_I4) {
-    if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_I4, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
-    else gg_tile_v4<V4Cfg<128>, QT_I4, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    if (cls == 0) gg_tile_v4_i4<V4Cfg<256>, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
+    else gg_tile_v4_i4<V4Cfg<128>, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
   } else if ((QM & (1 << QT_F16)) && mt.qtype == QT_F16) {
     if (cls == 0) gg_tile_v4<V4Cfg<256>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
     else if (cls == 1) gg_tile_v4<V4Cfg<128>, QT_F16, OPT>(mt, A, B, SA, SB, C, td.m0, td.n0, lds, sk);
