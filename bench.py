@@ -715,6 +715,17 @@ def main():
             torch.cuda.empty_cache()
         except Exception as e:  # noqa: BLE001 - an extra must not sink the headline line
             extras["moe_layer"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        try:  # the same layer at bs 512, where the gate_up call runs on the small-batch kernel (wo3)
+            from mxmoe_amd.moe import qwen2_layer_bench
+
+            extras["moe_layer_bs512"] = {
+                "what": "as moe_layer at bs 512; interleaved = the fused layout through the plain epilogue + the "
+                        "interleaved-input SiLU pass (the small-batch form before round 6, when wo3 had no SiLU "
+                        "epilogue)",
+                **qwen2_layer_bench(rounds=2, iters=20, bs=512, interleaved=True)}
+            torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001
+            extras["moe_layer_bs512"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         try:  # the same on the DeepSeek-V2-Lite mixed layer (64 routed experts, top-6, merged shared experts)
             from mxmoe_amd.moe import qwen2_layer_bench
 

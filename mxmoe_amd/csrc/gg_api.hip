@@ -85,6 +85,7 @@ struct Variant {
   int tail_bm;         // v2: height of the tail-tile class (0 = none)
   int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
   bool persistent = false;  // v2p / v2q: a workgroup walks a planned tile list
+  bool silu_epi = false;    // the fp16 / w8a8 / w4a4 tile bodies carry the fused SiLU epilogue
   int persist_len = 0;      // v2q: 0 = one list per CU (static); L > 0 = lists of L consecutive XCD-queue
                             // tiles, one per block, the hardware dispatching blocks as CUs free up
   int (*lds_of)(int qmask) = nullptr;  // LDS of the build a quant-type set launches (default lds_bytes)
@@ -282,6 +283,7 @@ Variant make_v3(const char* name) {
   v.k_stage_bytes = 0;
   v.tail_bm = 128;
   v.launch = &launch_v3<BN, WN, NBUF, DIST, OPT>;
+  v.silu_epi = true;  // epilogue_v3
   return v;
 }
 
@@ -335,6 +337,7 @@ template <int ABL = 0>
 Variant make_v2(const char* name) {
   Variant v = v2_base(name, (ABL & V2_B3) ? 160 * 1024 : V2Cfg<256>::LDS_BYTES + V2_LDS_EXTRA);
   v.launch = &launch_v2<ABL>;
+  v.silu_epi = true;  // gg_tile_v2's epilogue
   return v;
 }
 
@@ -357,6 +360,7 @@ Variant make_wo2(const char* name) {
   v.tail2_bm = 0;
   v.launch = &launch_wo2<ABL, NWG>;
   v.lds_of = &wo2_launch_lds<NWG>;
+  v.silu_epi = true;  // its fp16 / w8a8 / w4a4 problems run gg_tile_v2 64 x 128 bodies (their epilogue)
   return v;
 }
 
@@ -421,16 +425,11 @@ typedef TileCfg<128, 128, 2, 2, 2> T128x128;
 typedef TileCfg<256, 128, 2, 2, 1> T256x128;
 typedef TileCfg<128, 256, 2, 2, 1> T128x256;
 
-// the fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL) lives in the 256-row fp16 / w8a8 / w4a4 tile bodies
-// of the v2 / v3 kernels (gg_tile_v2, epilogue_v3); the small-batch wo3 kernel and the persistent
-// lab kernels have none (mxmoe_gg_variant_caps reports it)
-bool has_silu_epilogue(const Variant& v) {
-  if (v.kind != Kind::V2 && v.kind != Kind::V3) return false;
-  if (v.persistent) return false;
-  for (int q : {QT_F16, QT_I8, QT_I4})
-    if (v.geom[q].bm != 256) return false;
-  return true;
-}
+// the fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL) lives in the fp16 / w8a8 / w4a4 tile bodies of the
+// v2 / v3 kernels (gg_tile_v2, epilogue_v3) — the small-batch wo3 kernel's 64 x 128 bodies of those
+// types included (round 6); the persistent, v4d and fp6 lab kernels have none (mxmoe_gg_variant_caps
+// reports it). Weight-only problems never carry the flag (build_meta).
+bool has_silu_epilogue(const Variant& v) { return v.silu_epi && !v.persistent; }
 
 // Production variants (libmxmoe_gg.so): every one computes correct results. The lab build
 // (-DMXMOE_LAB -> libmxmoe_gg_lab.so, tools only: `python -m mxmoe_amd.build --lab`) compiles the
@@ -1436,9 +1435,8 @@ int resolve_variant(int variant, const std::vector<HostProblem>& hp, int* out) {
   *out = variant_index(kDefaultVariantName);
   const int wo_mask = (1 << QT_W4A16) | (1 << QT_W8A16) | (1 << QT_W2A16);
   const int small_mask = wo_mask | (1 << QT_I8) | (1 << QT_F16) | (1 << QT_I4);
-  bool any_silu = false;  // the small-batch kernel has no SiLU epilogue
-  for (const HostProblem& p : hp) any_silu = any_silu || (p.fmt & MXMOE_GG_EPI_SILU_MUL) != 0;
-  if (mask != 0 && (mask & ~small_mask) == 0 && !any_silu) {
+  // (fused SiLU calls too: the small-batch kernel's fp16 / w8a8 / w4a4 bodies carry the epilogue)
+  if (mask != 0 && (mask & ~small_mask) == 0) {
     // (w8a8 / fp16 problems may ride along: the reference's small-batch w4a16 + w8a8 pairing)
     double wsum0 = 0, ksum = 0;
     int kmax = 0;

@@ -435,9 +435,11 @@ class MoEFFN:
         (MXMOE_GG_EPI_SILU_MUL; gate_up weights stored with gate / up rows interleaved in 16-row
         blocks) and only the quantisation runs after it — bit-identical outputs, half the gate_up C
         bytes and no separate SiLU pass (qwen2_moe layer step -6 %). Needs every gate_up qcfg in
-        FUSE_QCFGS. None (default): fuse whenever the qcfgs allow. A call AUTO would hand to the
-        small-batch kernel (which has no SiLU epilogue) runs the plain epilogue on the interleaved
-        weights and the interleaved-input SiLU pass instead — same outputs, wo3's speed."""
+        FUSE_QCFGS. None (default): fuse whenever the qcfgs allow. A call whose kernel has no SiLU
+        epilogue (lab kernels; ``gate_up_mode = "interleaved"`` forces it) runs the plain epilogue on
+        the interleaved weights and the interleaved-input SiLU pass instead — same outputs. (Before
+        round 6 that was every small-batch call: the wo3 kernel's fp16 / w8a8 / w4a4 bodies now carry
+        the epilogue too.)"""
         self.E = num_routed
         self.has_shared = len(gate_up) == num_routed + 1
         self.H = gate_up[0].shape[1]
@@ -452,6 +454,7 @@ class MoEFFN:
         self.w2 = [prepare_weight(w, q[1]) for w, q in zip(down, qcfg)]
         self.tag1 = [qtag_of(q[0].a_bits, q[0].gsize) for q in qcfg]
         self.tag2 = [qtag_of(q[1].a_bits, q[1].gsize) for q in qcfg]
+        self.gate_up_mode: Optional[str] = None  # None: the library decides; "interleaved": A/B override
 
     def gate_up_call(self, a1: ActBatch, T: int, topk: int, dev):
         """The planned gate_up GroupGEMM of one call and its output buffers: (GroupGemm, h1, h1s, mode),
@@ -478,7 +481,9 @@ class MoEFFN:
             return ps, h1, h1s
 
         mode = "plain"
-        if self.fuse_silu:
+        if self.fuse_silu and self.gate_up_mode == "interleaved":
+            mode = "interleaved"
+        elif self.fuse_silu:
             ph = torch.empty(0, dtype=torch.float16, device=dev)
             probe = problems(lambda e, sg: ph, False)  # shapes only: AUTO's choice for the plain epilogue
             arr = (nat.GGProblemC * max(len(probe), 1))(*[p.to_c() for p in probe])
@@ -561,12 +566,15 @@ class PlannedForward:
         return self.out
 
 
-def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192, model: str = "qwen2_moe") -> dict:
+def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192, model: str = "qwen2_moe",
+                      interleaved: bool = False) -> dict:
     """qwen2_moe layer 11 (LP-1 mixed w4a4 + w8a8 qconfig, the committed routing histogram) — or
     model="ds2": the DeepSeek-V2-Lite mixed layer of the bench (64 routed experts, top-6, the two
     shared experts as one of twice the width) — with random weights, as planned MoE FFN steps,
     unfused vs the fused SiLU epilogue: per-stage and step device times (median over alternating
-    rounds, µs) and whether the two outputs are bit-identical."""
+    rounds, µs) and whether the two outputs are bit-identical. interleaved: a third step, the fused
+    layout through the plain epilogue + the interleaved-input SiLU pass (the small-batch form before
+    round 6), with each step's gate_up mode."""
     from .harness import time_launches
     from .workload import ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
 
@@ -592,13 +600,17 @@ def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192, model: s
     down.append(((torch.rand(H, Ns, generator=g) * 2 - 1) * 0.05).half().to(dev))
     hidden = ((torch.rand(bs, H, generator=g) * 2 - 1)).half().to(dev)
     wts = torch.softmax(torch.rand(bs, topk, generator=g), dim=1).to(dev)
-    steps = {name: PlannedForward(MoEFFN(gate_up, down, qcfg, num_routed=E, fuse_silu=fuse), hidden, ids, wts)
-             for name, fuse in (("unfused", False), ("fused", True))}
-    del gate_up, down
+    modes = [("unfused", False, None), ("fused", True, None)] + ([("interleaved", True, "interleaved")] if interleaved else [])
+    steps = {}
+    for name, fuse, override in modes:
+        layer_ = MoEFFN(gate_up, down, qcfg, num_routed=E, fuse_silu=fuse)
+        layer_.gate_up_mode = override
+        steps[name] = PlannedForward(layer_, hidden, ids, wts)
+    del gate_up, down, layer_
     for st in steps.values():
         st()
     torch.cuda.synchronize()
-    same = torch.equal(steps["unfused"].out.view(torch.int16), steps["fused"].out.view(torch.int16))
+    same = all(torch.equal(steps["unfused"].out.view(torch.int16), st.out.view(torch.int16)) for st in steps.values())
     res = {n: {"step": []} | {k: [] for k in st.stages} for n, st in steps.items()}
     for _ in range(rounds):
         for n, st in steps.items():
@@ -608,4 +620,7 @@ def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192, model: s
     out = {n: {k: round(sorted(v)[len(v) // 2] * 1e3, 1) for k, v in d.items()} for n, d in res.items()}
     out["bit_identical"] = bool(same)
     out["speedup"] = round(out["unfused"]["step"] / out["fused"]["step"], 4)
+    out["gate_up_mode"] = {n: st.mode for n, st in steps.items()}
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    out["gate_up_variant"] = {n: names[st.g1.variant] for n, st in steps.items()}
     return out

@@ -50,12 +50,14 @@ def test_abi_version_and_variants():
 
 
 def test_variant_caps_silu_epilogue():
-    """mxmoe_gg_variant_caps (ABI 7): the general kernels (v2x, v3) carry the fused SiLU epilogue, the
-    small-batch wo3 kernel does not — what MoEFFN.gate_up_call asks instead of matching names."""
+    """mxmoe_gg_variant_caps (ABI 7): every product kernel carries the fused SiLU epilogue — v2x, v3,
+    and (round 6) the small-batch wo3 kernel's fp16 / w8a8 / w4a4 bodies — what MoEFFN.gate_up_call
+    asks instead of matching names."""
     names = {ln.split()[1]: int(ln.split()[0]) for ln in nat.list_variants()}
+    assert set(names) >= {"v2x_256x256_w8_b3_buf_spread_edma", "v3_256x128_w4_dma_ring3_2wg", "wo3_64x256_w8_3wg"}
     for name, v in names.items():
         caps = nat.variant_caps(v)
-        assert bool(caps & nat.CAP_SILU_MUL) == (not name.startswith("wo")), name
+        assert caps & nat.CAP_SILU_MUL, name
     with pytest.raises(nat.GGError):
         nat.variant_caps(len(names))
 

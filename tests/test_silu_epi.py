@@ -2,8 +2,8 @@
 the slot quantiser behind it (mxmoe_moe_quant_slots, include/mxmoe_moe.h) — §8(f) rank 2, the MoE
 layer's silu_mul_then_quant (ref_bind.cu:595-757) folded into the GEMM that produces its input.
 
-CPU: the gate / up interleave, the ABI's validation of the flag (types, N % 32, variants, AUTO never
-handing a fused call to the small-batch kernel). GPU: fused outputs against the unfused call + the
+CPU: the gate / up interleave, the ABI's validation of the flag (types, N % 32, variants, AUTO
+handing small fused calls to the small-batch kernel, whose fp16 / w8a8 / w4a4 bodies carry it). GPU: fused outputs against the unfused call + the
 oracle SiLU (1 fp16 ulp, as the MoE plumbing tests), the slot quantiser against silu_mul_quant bit
 for bit, and MoEFFN with and without fusion returning bit-identical layers.
 """
@@ -56,8 +56,9 @@ def test_flag_validation():
         nat.workspace_size(_arr(_cp(64, 512, 256, W4A4_G128)), 1, v2x)
     with pytest.raises(nat.GGError, match="SiLU epilogue needs"):
         nat.workspace_size(_arr(_cp(64, 512, 256, QParams(16, 4, 128, False))), 1, v2x)
-    with pytest.raises(nat.GGError, match="no SiLU epilogue"):
-        nat.workspace_size(_arr(_cp(64, 512, 256, W8A8)), 1, wo3)
+    assert nat.workspace_size(_arr(_cp(64, 512, 256, W8A8), _cp(30, 512, 256, W4A4), _cp(9, 256, 128, FP16)), 3, wo3) > 0
+    with pytest.raises(nat.GGError, match="SiLU epilogue needs"):  # weight-only problems never carry it
+        nat.workspace_size(_arr(_cp(64, 512, 256, QParams(16, 4, 128, False))), 1, wo3)
     with pytest.raises(nat.GGError, match="ldc"):
         nat.workspace_size(_arr(_cp(64, 512, 256, W8A8, ldc=200)), 1, v2x)
     assert nat.workspace_size(_arr(_cp(64, 512, 256, W8A8, ldc=256)), 1, v2x) > 0  # ldc >= N / 2 suffices
@@ -65,11 +66,11 @@ def test_flag_validation():
     bad.fmt |= 0x200
     with pytest.raises(nat.GGError, match="unknown fmt flags"):
         nat.workspace_size(_arr(bad), 1, v2x)
-    # small batch: AUTO would take wo3 for the plain call, never for the fused one
+    # small batch: AUTO takes wo3 for the plain call and for the fused one alike (round 6)
     small = [_cp(30, 2816, 2048, W8A8, silu=False) for _ in range(8)]
     assert names[nat.resolve_variant(_arr(*small), 8)] == "wo3_64x256_w8_3wg"
     fused = [_cp(30, 2816, 2048, W8A8) for _ in range(8)]
-    assert names[nat.resolve_variant(_arr(*fused), 8)] != "wo3_64x256_w8_3wg"
+    assert names[nat.resolve_variant(_arr(*fused), 8)] == "wo3_64x256_w8_3wg"
     # w4a4-only calls keep their kernel (v3 has the epilogue too)
     assert names[nat.resolve_variant(_arr(_cp(4096, 2816, 2048, W4A4)), 1)] == "v3_256x128_w4_dma_ring3_2wg"
 
@@ -105,7 +106,8 @@ def _gate_up_problem(M, Nh, K, q, seed, ldc=0):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("q", [FP16, W8A8, W4A4], ids=["fp16", "w8a8", "w4a4"])
-@pytest.mark.parametrize("vname", ["v2x_256x256_w8_b3_buf_spread_edma", "v3_256x128_w4_dma_ring3_2wg", "auto"])
+@pytest.mark.parametrize("vname", ["v2x_256x256_w8_b3_buf_spread_edma", "v3_256x128_w4_dma_ring3_2wg", "wo3_64x256_w8_3wg",
+                                   "auto"])
 def test_fused_epilogue_matches_unfused_plus_silu(gpu, q, vname):
     names = [ln.split()[1] for ln in nat.list_variants()]
     variant = None if vname == "auto" else names.index(vname)
@@ -161,11 +163,12 @@ def test_quant_slots_equals_silu_mul_quant(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T,mode", [(60, "interleaved"), (200, "fused"), (2048, "fused")])
-def test_moe_ffn_fused_equals_unfused(gpu, T, mode):
-    """A fused-layout layer equals the plain one bit for bit; at T = 60 AUTO would send the plain
-    gate_up call to wo3, so the layer runs the interleaved weights through the plain epilogue and
-    the interleaved-input SiLU pass (mxmoe_moe_silu_mul_quant_il) instead."""
+@pytest.mark.parametrize("T,override,variant", [(60, None, "wo3_64x256_w8_3wg"), (60, "interleaved", "wo3_64x256_w8_3wg"),
+                                               (200, None, None), (2048, None, None)])
+def test_moe_ffn_fused_equals_unfused(gpu, T, override, variant):
+    """A fused-layout layer equals the plain one bit for bit; at T = 60 the gate_up call runs on wo3
+    (its fused epilogue since round 6), and with the "interleaved" override the interleaved weights
+    go through the plain epilogue and the interleaved-input SiLU pass (mxmoe_moe_silu_mul_quant_il)."""
     topk, E, H, N, Ns = 4, 6, 256, 384, 768
     g = torch.Generator().manual_seed(21)
     gate_up = [((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half() for _ in range(E)]
@@ -177,6 +180,8 @@ def test_moe_ffn_fused_equals_unfused(gpu, T, mode):
     plain = moe.MoEFFN(gu, dn, qcfg, num_routed=E, fuse_silu=False)
     fused = moe.MoEFFN(gu, dn, qcfg, num_routed=E)  # (default: fused when every gate_up qcfg allows)
     assert fused.fuse_silu
+    fused.gate_up_mode = override
+    mode = override or "fused"
     logits = torch.rand(T, E, generator=g)
     ids = torch.topk(logits, topk, dim=1).indices.to(torch.int32).to(DEV)
     wts = torch.softmax(torch.rand(T, topk, generator=g), dim=1).to(DEV)
@@ -186,7 +191,10 @@ def test_moe_ffn_fused_equals_unfused(gpu, T, mode):
     torch.cuda.synchronize()
     assert torch.equal(m1["a2"].out, m2["a2"].out) and torch.equal(m1["a2"].scales, m2["a2"].scales)
     assert torch.equal(o1.view(torch.int16), o2.view(torch.int16))
-    assert moe.PlannedForward(fused, h, ids, wts).mode == mode
+    step = moe.PlannedForward(fused, h, ids, wts)
+    assert step.mode == mode
+    if variant:
+        assert [ln.split()[1] for ln in nat.list_variants()][step.g1.variant] == variant
     with pytest.raises(ValueError, match="fuse_silu"):
         moe.MoEFFN(gu, dn, [(W4A4_G128, W8A8)] + qcfg[1:], num_routed=E, fuse_silu=True)
 
