@@ -157,3 +157,23 @@ def assert_fakequant_close(out: np.ndarray, ref_fq: np.ndarray, what: str = ""):
     rms = nref / np.sqrt(ref.size)
     bad = np.abs(out - ref) > 1e-3 * np.abs(ref) + 4e-3 * rms
     assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} outputs outside the fake-quant tolerance"
+
+
+def codes_f64(packed: torch.Tensor, rows: int, bits: int, K: int) -> torch.Tensor:
+    """pack_wxax rows -> their integer codes as f64 [rows, K]. The codes come out in the packed byte /
+    nibble order (pack_wxax puts element 0 of each 16-bit word in its high bits, oracle/gg_oracle.c
+    unpack_row), the same permutation of K for A and B, which leaves every dot product unchanged."""
+    b = packed.contiguous().view(torch.int8).view(rows, -1)[:, :K * bits // 8]
+    if bits == 8:
+        return b.double()
+    lo = torch.bitwise_right_shift(torch.bitwise_left_shift(b, 4), 4)  # sign-extended low nibble
+    hi = torch.bitwise_right_shift(b, 4)                               # (arithmetic shift)
+    return torch.stack((lo, hi), dim=-1).view(rows, -1).double()
+
+
+def quant_epilogue_ref(acc, sa, sb):
+    """oracle_gg_quant's epilogue on a whole f64 accumulator matrix (torch, any device):
+    fp16_rn(0 + f32(acc) * f32(fp16_rn(sa[m] * sb[n]))) — the fp16 product of two fp16 scales is
+    exact in f32 and rounded once, f32(acc) and the f32 product round to nearest, +0 turns -0 into +0."""
+    s16 = sa.view(-1, 1).half() * sb.view(1, -1).half()
+    return (acc.float() * s16.float() + 0.0).half()

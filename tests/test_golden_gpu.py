@@ -2,7 +2,11 @@
 
 Also runs the full-size qwen2_moe layer-11 (bs=8192) GroupGEMMs and checks size-independent
 properties: exact agreement with the oracle on a random sample of rows x columns of every problem
-(C[rows, cols] only depends on A[rows] and B[cols]), and determinism across launches.
+(C[rows, cols] only depends on A[rows] and B[cols]), and determinism across launches; and, for the
+kernel AUTO benches, EVERY output of every problem against an exhaustive restatement of the oracle's
+arithmetic on the GPU (round 6): the integer dot products as f64 GEMMs (exact: |acc| < 2^53), the
+oracle's epilogue in torch's IEEE fp16 / fp32 operations, bit for bit; fp16 against an f64 GEMM
+within the fp16 tolerance.
 """
 from __future__ import annotations
 
@@ -15,7 +19,8 @@ import torch
 from mxmoe_amd import _native as nat
 from mxmoe_amd.groupgemm import GroupGemm, Problem, QParams, group_gemm
 from oracle import oracle
-from tests._util import FULL_SIZE_CFGS, assert_f16_close, full_size_layer, full_size_variants
+from tests._util import (FULL_SIZE_CFGS, assert_f16_close, codes_f64, full_size_layer, full_size_variants,
+                         quant_epilogue_ref)
 
 pytestmark = pytest.mark.gpu
 GOLD = Path(__file__).resolve().parent / "golden"
@@ -123,3 +128,54 @@ def test_full_size_layer11_sampled_parity(cfg, variant):
             assert torch.equal(a.view(torch.int16), p.C.view(torch.int16))
         del inp, ggm
         torch.cuda.empty_cache()
+
+
+def _exhaustive_check(inputs):
+    """Every output of every problem. w8a8 / w4a4: acc = exact integer dot product (f64 GEMM of the
+    codes), then the oracle's epilogue fp16_rn(0 + f32(acc) * f32(fp16_rn(sa[m] * sb[n])))
+    (oracle_gg_quant) as torch IEEE operations — compared bit for bit. fp16: an f64 GEMM, within the
+    fp16 tolerance of tests/_util.assert_f16_close."""
+    for p in inputs.problems:
+        if p.M == 0:
+            continue
+        out = p.C[:p.M, :p.N]
+        if p.q.is_quant:
+            assert p.q.gsize == -1 and p.q.a_bits == p.q.w_bits, p.q.qcfg
+            bits = p.q.a_bits
+            acc = codes_f64(p.A, p.M, bits, p.K) @ codes_f64(p.B, p.N, bits, p.K).T
+            assert float(acc.abs().max()) < 2.0 ** 31
+            ref = quant_epilogue_ref(acc, p.scale_a[:p.M], p.scale_b[:p.N])
+            del acc
+            same = out.contiguous().view(torch.int16) == ref.view(torch.int16)
+            assert bool(same.all()), f"{p.q.qcfg} M={p.M} N={p.N} K={p.K}: {int((~same).sum())} outputs differ"
+        else:
+            ref = p.A[:p.M].double() @ p.B[:p.N].double().T
+            o = out.double()
+            assert bool(torch.isfinite(o).all())
+            rms = float(ref.square().mean().sqrt())
+            bad = (o - ref).abs() > 1e-3 * ref.abs() + 1e-3 * rms + 1e-6
+            assert not bool(bad.any()), f"fp16 M={p.M} N={p.N} K={p.K}: {int(bad.sum())} outputs outside tolerance"
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cfg", FULL_SIZE_CFGS)
+def test_full_size_layer11_exhaustive_parity(cfg):
+    """BASELINE configs[1]-[4] at full size through AUTO (the benched kernels): every output checked
+    (not a sample) — the restated oracle arithmetic above, on the GPU."""
+    from mxmoe_amd.harness import build_layer_inputs
+
+    wl = full_size_layer(cfg)
+    for gg in ("gate_up", "down"):
+        inp = build_layer_inputs(wl[gg])
+        GroupGemm(inp.problems).launch()
+        torch.cuda.synchronize()
+        _exhaustive_check(inp)
+        # the check is not vacuous: one output of the largest problem with an exponent bit flipped fails it
+        big = max(inp.problems, key=lambda q: q.M * q.N)
+        r, c = big.M - 1, big.N // 3
+        big.C.view(torch.int16)[r, c] ^= 0x2000
+        with pytest.raises(AssertionError):
+            _exhaustive_check(type(inp)(problems=[big], shapes=None))
+        del inp
+        torch.cuda.empty_cache()
+

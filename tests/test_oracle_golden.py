@@ -94,3 +94,31 @@ def test_f32_to_f16_rounding_matches_numpy():
     lib = oracle.lib()
     got = np.array([lib.oracle_f32_to_f16(float(v)) for v in x.astype(np.float32)], dtype=np.uint16)
     assert (got == x.astype(np.float16).view(np.uint16)).all()
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+def test_exhaustive_restatement_matches_oracle(bits):
+    """The GPU exhaustive parity check's restatement (tests/_util.codes_f64 + quant_epilogue_ref: f64
+    GEMM of the packed codes, the epilogue as torch IEEE ops) equals oracle_gg_quant bit for bit,
+    including zero accumulators, extreme codes and scales that overflow fp16."""
+    from tests._util import codes_f64, quant_epilogue_ref
+
+    rng = np.random.default_rng(bits)
+    M, N, K = 37, 45, 512
+    qmax = (1 << (bits - 1)) - 1
+    qa = rng.integers(-qmax, qmax + 1, (M, K)).astype(np.int8)
+    qb = rng.integers(-qmax, qmax + 1, (N, K)).astype(np.int8)
+    qa[0] = 0                     # zero accumulators (+0, never -0)
+    qa[1], qb[1] = qmax, -qmax    # extreme sums
+    A = pack_wxax(torch.from_numpy(qa), bits).view(torch.uint8).numpy()
+    B = pack_wxax(torch.from_numpy(qb), bits).view(torch.uint8).numpy()
+    sa = (rng.random(M) * 0.02 + 1e-4).astype(np.float16)
+    sb = (rng.random(N) * 0.02 + 1e-4).astype(np.float16)
+    sa[2], sb[3] = 60000.0, 60000.0  # fp16_rn(sa * sb) = inf on row 2 x column 3
+    ref = oracle.gg_quant(A, B, sa, sb, M, N, K, bits)
+    acc = codes_f64(torch.from_numpy(A), M, bits, K) @ codes_f64(torch.from_numpy(B), N, bits, K).T
+    assert torch.equal(acc, torch.from_numpy(qa.astype(np.float64) @ qb.astype(np.float64).T))
+    got = quant_epilogue_ref(acc, torch.from_numpy(sa), torch.from_numpy(sb)).numpy()
+    g16, r16 = got.view(np.uint16), ref.view(np.uint16)
+    both_nan = np.isnan(got) & np.isnan(ref)
+    assert ((g16 == r16) | both_nan).all()
