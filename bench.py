@@ -726,6 +726,15 @@ def main():
             torch.cuda.empty_cache()
         except Exception as e:  # noqa: BLE001
             extras["moe_layer_bs512"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        try:  # the reference's small-batch MoE scheme (w4a16 experts + 1/16 w8a8) at bs 512: the weight-only
+            # gate_up problems take wo3's WO_SILU build when fused
+            from mxmoe_amd.moe import qwen2_layer_bench
+
+            extras["moe_layer_w4a16_w8a8_bs512"] = qwen2_layer_bench(rounds=2, iters=20, bs=512, interleaved=True,
+                                                                     scheme="w4a16_w8a8")
+            torch.cuda.empty_cache()
+        except Exception as e:  # noqa: BLE001
+            extras["moe_layer_w4a16_w8a8_bs512"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         try:  # the same on the DeepSeek-V2-Lite mixed layer (64 routed experts, top-6, merged shared experts)
             from mxmoe_amd.moe import qwen2_layer_bench
 

@@ -62,8 +62,9 @@ enum {
   MXMOE_GG_FMT_BF16 = 2     /* bf16: 16-bit operands are bfloat16                              */
 };
 
-/* Epilogue flag, OR-ed into mxmoe_gg_problem.fmt (fp16, w8a8_g-1_sym and w4a4_g-1_sym problems, v2x
- * and v3 variants; no reference counterpart — it fuses the MoE layer's silu_mul_then_quant
+/* Epilogue flag, OR-ed into mxmoe_gg_problem.fmt (fp16, w8a8_g-1_sym and w4a4_g-1_sym problems on the
+ * v2x, v3 and wo3 variants; weight-only WxA16 problems on wo3, whose scale_b is permuted with the rows;
+ * no reference counterpart — it fuses the MoE layer's silu_mul_then_quant
  * activation, ref_bind.cu:595-757, into the gate_up GroupGEMM). B holds N = 2 Nh rows interleaved
  * in 16-row blocks: rows [32 b, 32 b + 16) are gate rows [16 b, 16 b + 16) and rows
  * [32 b + 16, 32 b + 32) the matching up rows (scale_b permuted alike; N % 32 == 0). C is [M][Nh]
@@ -113,7 +114,8 @@ typedef struct mxmoe_gg_plan_info {
   int32_t block;
   int32_t lds_bytes;
   int32_t qtype_mask;      /* bit q set if a planned problem has quant type q (0 fp16, 1 w8a8, 2 w4a4,
-                            * 3 w4a16, 4 w8a16, 5 w4a4_g128, 6 w2a16, 7 w8a8 E4M3, 8 bf16);
+                            * 3 w4a16, 4 w8a16, 5 w4a4_g128, 6 w2a16, 7 w8a8 E4M3, 8 bf16); bit 16:
+                            * a weight-only problem carries MXMOE_GG_EPI_SILU_MUL (small-batch kernel);
                             * selects the kernel specialisation at launch */
   int32_t splitk_slabs;    /* 256-KiB partial-sum slabs the plan's split-K tiles use (0: no split) */
   int64_t workspace_bytes; /* bytes of the workspace actually used by the plan */

@@ -86,6 +86,7 @@ struct Variant {
   int tail2_bm = 0;    // v2: height of the small-remainder class (0 = none)
   bool persistent = false;  // v2p / v2q: a workgroup walks a planned tile list
   bool silu_epi = false;    // the fp16 / w8a8 / w4a4 tile bodies carry the fused SiLU epilogue
+  bool silu_wo = false;     // ... and its weight-only tiles (wo2: the WO_SILU builds)
   int persist_len = 0;      // v2q: 0 = one list per CU (static); L > 0 = lists of L consecutive XCD-queue
                             // tiles, one per block, the hardware dispatching blocks as CUs free up
   int (*lds_of)(int qmask) = nullptr;  // LDS of the build a quant-type set launches (default lds_bytes)
@@ -221,8 +222,15 @@ void launch_wo2_q(const GGArgs& a, int grid, hipStream_t s) {
 // quant-type sets launched at the variant's NWG (the rest, with 8-bit weight-only problems, run the
 // 2-WG/CU build): keep in step with the switch below
 constexpr bool wo2_full_nwg(int qm) { return qm == 8 || qm == 64 || qm == 10 || qm == 1 || qm == 2 || qm == 4 || qm == 6; }
+// plan-info qtype_mask bit: a weight-only problem carries MXMOE_GG_EPI_SILU_MUL (selects the WO_SILU
+// build; with it only the w4a16 and w4a16 + w8a8 sets run at the variant's NWG)
+constexpr int kQmaskWoSilu = 1 << 16;
+constexpr bool wo2_full_nwg_silu(int qm) { return qm == 8 || qm == 10; }
 template <int NWG>
-int wo2_launch_lds(int qmask) { return wo2_full_nwg(qmask & 511) ? wo2_lds_bytes<NWG>() : wo2_lds_bytes<2>(); }
+int wo2_launch_lds(int qmask) {
+  const bool full = (qmask & kQmaskWoSilu) ? wo2_full_nwg_silu(qmask & 511) : wo2_full_nwg(qmask & 511);
+  return full ? wo2_lds_bytes<NWG>() : wo2_lds_bytes<2>();
+}
 template <int ABL, int NWG>
 void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
 #ifdef MXMOE_LAB_FAST
@@ -235,6 +243,16 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
       abort();
   }
 #else
+  if (qmask & kQmaskWoSilu) {  // weight-only problems with the fused SiLU epilogue (WO_SILU builds)
+    constexpr int AS = ABL | WO_SILU;
+    switch (qmask & 511) {
+      case 8: launch_wo2_q<AS, 8, NWG>(a, grid, s); break;    // w4a16 (+ fp16 / w8a8 / w4a4 riding along
+      case 10: launch_wo2_q<AS, 10, NWG>(a, grid, s); break;  // take the wide build below)
+      case 16: launch_wo2_q<AS, 16, 2>(a, grid, s); break;
+      default: launch_wo2_q<AS, 95, 2>(a, grid, s); break;
+    }
+    return;
+  }
   switch (qmask & 511) {
     case 8: launch_wo2_q<ABL, 8, NWG>(a, grid, s); break;    // w4a16 only
     case 64: launch_wo2_q<ABL, 64, NWG>(a, grid, s); break;  // w2a16 only
@@ -361,6 +379,9 @@ Variant make_wo2(const char* name) {
   v.launch = &launch_wo2<ABL, NWG>;
   v.lds_of = &wo2_launch_lds<NWG>;
   v.silu_epi = true;  // its fp16 / w8a8 / w4a4 problems run gg_tile_v2 64 x 128 bodies (their epilogue)
+#ifndef MXMOE_LAB_FAST
+  v.silu_wo = true;   // weight-only problems: the WO_SILU builds (launch_wo2)
+#endif
   return v;
 }
 
@@ -672,13 +693,16 @@ int build_meta_weightonly(const HostProblem& p, int idx, int qt, const Variant& 
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: weight-only group size %d must be -1 or a multiple of 64 dividing K=%d",
                 idx, p.gsize, p.K);
   if (p.N % 8 != 0) return fail(MXMOE_GG_ERR_INVALID, "problem %d: N=%d must be a multiple of 8", idx, p.N);
+  const bool silu = (p.fmt & MXMOE_GG_EPI_SILU_MUL) != 0;  // (build_meta checked N % 32 and the variant)
   const int64_t arow = (int64_t)p.K * 2, brow = (int64_t)p.K * p.w_bits / 8;
   const int64_t lda_b = p.lda ? p.lda * 2 : arow;
   const int64_t ldb_b = p.ldb ? p.ldb * 2 : brow;
-  const int64_t ldc = p.ldc ? p.ldc : p.N;
+  const int64_t ncols = silu ? p.N / 2 : p.N;  // columns of C
+  const int64_t ldc = p.ldc ? p.ldc : ncols;
   if (lda_b < arow || ldb_b < brow || (lda_b % 16) || (ldb_b % 16))
     return fail(MXMOE_GG_ERR_INVALID, "problem %d: lda/ldb must be >= K row and a multiple of 8 words", idx);
-  if (ldc < p.N || (ldc % 8)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= N and a multiple of 8", idx);
+  if (ldc < ncols || (ldc % 8))
+    return fail(MXMOE_GG_ERR_INVALID, "problem %d: ldc must be >= %s and a multiple of 8", idx, silu ? "N / 2" : "N");
   if (check_ptrs && p.M > 0 && p.N > 0) {
     if (!p.A || !p.B || !p.C) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL A/B/C", idx);
     if (!p.SB) return fail(MXMOE_GG_ERR_INVALID, "problem %d: NULL scale pointer (weight-only scale_b)", idx);
@@ -695,7 +719,7 @@ int build_meta_weightonly(const HostProblem& p, int idx, int qt, const Variant& 
   m->tiles_n = (p.N + v.geom[qt].bn - 1) / v.geom[qt].bn;
   m->kbytes = (int32_t)arow;
   m->reserved = p.gsize == -1 ? std::max(1, p.K / 64) : p.gsize / 64;  // 64-K stages per scale group
-  m->reserved2 = p.sym ? 1 : 0;
+  m->reserved2 = (p.sym ? 1 : 0) | (silu ? META_SILU : 0);
   m->lda_b = lda_b;
   m->ldb_b = ldb_b;
   m->ldc = ldc;
@@ -712,8 +736,10 @@ int build_meta(const HostProblem& p, int idx, const Variant& v, bool check_ptrs,
                 idx, v.name, p.w_bits, p.a_bits);
   const bool silu = (p.fmt & MXMOE_GG_EPI_SILU_MUL) != 0;
   if (p.fmt & ~(0xFF | MXMOE_GG_EPI_SILU_MUL)) return fail(MXMOE_GG_ERR_INVALID, "problem %d: unknown fmt flags %#x", idx, p.fmt);
-  if (silu && !(qt == QT_F16 || qt == QT_I8 || qt == QT_I4))
-    return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: the SiLU epilogue needs fp16, w8a8_g-1_sym or w4a4_g-1_sym", idx);
+  if (silu && !(qt == QT_F16 || qt == QT_I8 || qt == QT_I4 || (is_weightonly(qt) && v.silu_wo)))
+    return fail(MXMOE_GG_ERR_UNSUPPORTED,
+                "problem %d: the SiLU epilogue needs fp16, w8a8_g-1_sym or w4a4_g-1_sym (weight-only: the small-batch "
+                "kernel wo3)", idx);
   if (silu && !has_silu_epilogue(v))
     return fail(MXMOE_GG_ERR_UNSUPPORTED, "problem %d: variant %s has no SiLU epilogue", idx, v.name);
   if (silu && p.N % 32) return fail(MXMOE_GG_ERR_INVALID, "problem %d: the SiLU epilogue needs N %% 32 == 0 (N=%d)", idx, p.N);
@@ -1534,7 +1560,10 @@ void fill_info(const Plan& plan, int variant, const WsLayout& l, void* ws, mxmoe
   info->reserved = 0;
   info->block = v.threads;
   info->qtype_mask = 0;
-  for (const GGMeta& m : plan.meta) info->qtype_mask |= 1 << m.qtype;
+  for (const GGMeta& m : plan.meta) {
+    info->qtype_mask |= 1 << m.qtype;
+    if (is_weightonly(m.qtype) && (m.reserved2 & META_SILU)) info->qtype_mask |= kQmaskWoSilu;
+  }
   info->lds_bytes = v.lds_of ? v.lds_of(info->qtype_mask) : v.lds_bytes;
   info->splitk_slabs = plan.slabs;
   info->workspace_bytes = (int64_t)l.total;

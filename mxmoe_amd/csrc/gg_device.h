@@ -702,6 +702,11 @@ enum : int {
   WO_BUF = 16
 };
 constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
+// weight-only option (round 6): the fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL, epilogue_v3's SiLU
+// path) compiled into gg_tile_wo — a separate wo2 instantiation, launched only for calls whose
+// weight-only problems carry the flag, so the plain 3-WG/CU build keeps its registers (the bit is
+// V2_EPIPE's, a v2 epilogue option no weight-only tile sees)
+constexpr int WO_SILU = 1 << 28;
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
 
 // Tile timeline (diagnostics, V2_TRACE builds only): per block {start, mainloop end, end (stores
@@ -2278,7 +2283,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
   const int64_t lda = mt.lda_b, ldb = mt.ldb_b;
   const int nst = sk.nst, ks0 = sk.ks0;  // 64-K stages [ks0, ks0 + nst) of this tile
   const int gstages = mt.reserved;  // stages per scale group (>= nst: one group)
-  const bool sym = mt.reserved2 != 0;
+  const bool sym = (mt.reserved2 & 1) != 0;  // (bit META_SILU: the fused SiLU epilogue)
 
   const uint8_t* srcA[GA];
   const uint8_t* srcB[GBW];
@@ -2728,7 +2733,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     lds_barrier();  // ring -> epilogue staging
   }
   if (!splitk_reduce<Cfg::NT>(acc, sk, lds)) return;  // split-K: only the last slice writes C
-  epilogue_v3<Cfg, QT_F16, false>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
+  epilogue_v3<Cfg, QT_F16, (WABL & WO_SILU) != 0>(mt, acc, nullptr, nullptr, C, m0, n0, lds);
 }
 
 template <int ABL, int QM>  // QM: quant types compiled in (bit 1 << QType), as gg_v3_kernel
@@ -2843,7 +2848,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | WO_BUF | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | WO_BUF | WO_SILU | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64

@@ -427,7 +427,10 @@ class MoEFFN:
     gate_up, QParams of down) — the activation side (a_bits, gsize) of each QParams sets how the
     plumbing quantises that expert's input (qtag_of). Expert E (if given) is the shared expert."""
 
-    FUSE_QCFGS = ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym")  # gate_up qcfgs with the SiLU epilogue
+    # gate_up qcfgs with the SiLU epilogue: fp16 / w8a8 / w4a4 on every product kernel, weight-only
+    # on the small-batch kernel (wo3; a large call of those falls back to the interleaved form)
+    FUSE_QCFGS = ("fp16", "w8a8_g-1_sym", "w4a4_g-1_sym")
+    FUSE_WEIGHT_ONLY = True
 
     def __init__(self, gate_up: Sequence[torch.Tensor], down: Sequence[torch.Tensor],
                  qcfg: Sequence[tuple[QParams, QParams]], num_routed: int, fuse_silu: Optional[bool] = None):
@@ -446,7 +449,7 @@ class MoEFFN:
         self.N = gate_up[0].shape[0] // 2
         self.Ns = gate_up[-1].shape[0] // 2 if self.has_shared else 0
         self.qcfg = list(qcfg)
-        eligible = all(q[0].qcfg in self.FUSE_QCFGS for q in qcfg)
+        eligible = all(q[0].qcfg in self.FUSE_QCFGS or (self.FUSE_WEIGHT_ONLY and q[0].is_weight_only) for q in qcfg)
         if fuse_silu and not eligible:
             raise ValueError(f"fuse_silu needs every gate_up qcfg in {self.FUSE_QCFGS}")
         self.fuse_silu = eligible if fuse_silu is None else fuse_silu
@@ -567,21 +570,24 @@ class PlannedForward:
 
 
 def qwen2_layer_bench(rounds: int = 4, iters: int = 30, bs: int = 8192, model: str = "qwen2_moe",
-                      interleaved: bool = False) -> dict:
+                      interleaved: bool = False, scheme: str = "lp1") -> dict:
     """qwen2_moe layer 11 (LP-1 mixed w4a4 + w8a8 qconfig, the committed routing histogram) — or
     model="ds2": the DeepSeek-V2-Lite mixed layer of the bench (64 routed experts, top-6, the two
     shared experts as one of twice the width) — with random weights, as planned MoE FFN steps,
     unfused vs the fused SiLU epilogue: per-stage and step device times (median over alternating
     rounds, µs) and whether the two outputs are bit-identical. interleaved: a third step, the fused
     layout through the plain epilogue + the interleaved-input SiLU pass (the small-batch form before
-    round 6), with each step's gate_up mode."""
+    round 6), with each step's gate_up mode. scheme (qwen2_moe): "lp1" (the LP-1 mixed w4a4 + w8a8
+    qconfig) or "w4a16_w8a8" (the reference's small-batch scheme, hz_fused.cuh:14-125)."""
     from .harness import time_launches
-    from .workload import ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload
+    from .workload import (ds2_mixed_qconfig, ds2_workload, load_workload, mixed_qconfig_lp1, qwen2_layer11_workload,
+                           w4a16_w8a8_qconfig)
 
     if model == "ds2":
         layer = load_workload(ds2_workload(bs, qconfig=ds2_mixed_qconfig()))["layer-1"]
     else:
-        layer = load_workload(qwen2_layer11_workload(bs, qconfig=mixed_qconfig_lp1()))["layer-11"]
+        qc = w4a16_w8a8_qconfig() if scheme == "w4a16_w8a8" else mixed_qconfig_lp1()
+        layer = load_workload(qwen2_layer11_workload(bs, qconfig=qc))["layer-11"]
     E = len(layer["gate_up"]) - 1
     H = layer["gate_up"][0].K
     N, Ns = layer["down"][0].K, layer["down"][-1].K

@@ -57,8 +57,8 @@ def test_flag_validation():
     with pytest.raises(nat.GGError, match="SiLU epilogue needs"):
         nat.workspace_size(_arr(_cp(64, 512, 256, QParams(16, 4, 128, False))), 1, v2x)
     assert nat.workspace_size(_arr(_cp(64, 512, 256, W8A8), _cp(30, 512, 256, W4A4), _cp(9, 256, 128, FP16)), 3, wo3) > 0
-    with pytest.raises(nat.GGError, match="SiLU epilogue needs"):  # weight-only problems never carry it
-        nat.workspace_size(_arr(_cp(64, 512, 256, QParams(16, 4, 128, False))), 1, wo3)
+    # weight-only problems carry it on wo3 only (its WO_SILU builds)
+    assert nat.workspace_size(_arr(_cp(64, 512, 256, QParams(16, 4, 128, False)), _cp(9, 256, 128, W8A8)), 2, wo3) > 0
     with pytest.raises(nat.GGError, match="ldc"):
         nat.workspace_size(_arr(_cp(64, 512, 256, W8A8, ldc=200)), 1, v2x)
     assert nat.workspace_size(_arr(_cp(64, 512, 256, W8A8, ldc=256)), 1, v2x) > 0  # ldc >= N / 2 suffices
@@ -233,3 +233,101 @@ def test_planned_forward_graph_replay(gpu):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(step.out.view(torch.int16), eager.view(torch.int16))
+
+
+WO_QS = [QParams(16, 4, -1, False), QParams(16, 4, 128, False), QParams(16, 4, 128, True), QParams(16, 8, -1, False),
+         QParams(16, 2, 128, False)]
+
+
+def _wo_gate_up_problem(M, Nh, K, q, seed, ldc=0):
+    """Weight-only unfused / fused problems over the same weights: the fused B is the gate_up weight
+    interleaved BEFORE quantisation (per-row groups commute with the row order, as MoEFFN does)."""
+    from mxmoe_amd.quantize import pack_weightonly_mi355x, quant_weightonly
+
+    g = torch.Generator().manual_seed(seed)
+    a = ((torch.rand(M, K, generator=g) * 2 - 1)).half().to(DEV)
+    w = ((torch.rand(2 * Nh, K, generator=g) * 2 - 1) * 0.25).half().to(DEV)
+
+    def packed(wt):
+        codes, sz = quant_weightonly(wt, q.w_bits, q.gsize, q.sym)
+        return pack_weightonly_mi355x(codes, q.w_bits), sz
+
+    B, sz = packed(w)
+    Bi, szi = packed(interleave_gate_up(w)[0])
+    C = torch.empty(max(M, 1), 2 * Nh, dtype=torch.float16, device=DEV)
+    plain = Problem(A=a, B=B, C=C, M=M, N=2 * Nh, K=K, q=q, scale_b=sz)
+    Cf = torch.full((max(M, 1), ldc or Nh), float("nan"), dtype=torch.float16, device=DEV)
+    fused = Problem(A=a, B=Bi, C=Cf, M=M, N=2 * Nh, K=K, q=q, scale_b=szi, silu=True, ldc=ldc)
+    return plain, fused
+
+
+def _check_fused(pairs, shapes):
+    for (p, f), (M, Nh, K) in zip(pairs, shapes):
+        if M == 0:
+            continue
+        ref = moe_ref.silu_mul(p.C[:M].cpu().numpy())
+        out = f.C[:M, :Nh].cpu().numpy()
+        assert np.isfinite(out).all()
+        d = np.abs(out.view(np.uint16).astype(np.int32) - ref.view(np.uint16).astype(np.int32))
+        same_sign = (np.signbit(out) == np.signbit(ref)) | (out == 0) | (ref == 0)
+        assert same_sign.all() and (d <= 1).all(), f"{p.q.qcfg} M={M} Nh={Nh} K={K}: {int((d > 1).sum())} outputs > 1 ulp"
+        if f.C.shape[1] > Nh:
+            assert torch.isnan(f.C[:M, Nh:]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", WO_QS, ids=[q.qcfg for q in WO_QS])
+def test_fused_epilogue_weight_only_on_wo3(gpu, q):
+    """Weight-only gate_up problems through the small-batch kernel's WO_SILU build (round 6): the
+    fused outputs within 1 fp16 ulp of the oracle SiLU of the unfused call's outputs; edge shapes, a
+    strided C, an empty problem, and a w8a8 problem with the flag in the same launch."""
+    names = [ln.split()[1] for ln in nat.list_variants()]
+    wo3 = names.index("wo3_64x256_w8_3wg")
+    shapes = [(35, 256, 256), (70, 1408, 512), (1, 128, 128), (129, 512, 384), (0, 256, 256), (64, 128, 1024),
+              (200, 384, 256)]
+    pairs = [_wo_gate_up_problem(M, Nh, K, q, seed=60 + i, ldc=(Nh + 24 if i == 6 else 0))
+             for i, (M, Nh, K) in enumerate(shapes)]
+    pairs.append(_gate_up_problem(48, 256, 512, W8A8, seed=99))
+    shapes.append((48, 256, 512))
+    GroupGemm([p for p, _ in pairs], variant=wo3).launch()
+    gg = GroupGemm([f for _, f in pairs])  # AUTO: the small-batch kernel, with the flag
+    assert names[gg.variant] == "wo3_64x256_w8_3wg"
+    assert gg.info.qtype_mask & (1 << 16)
+    gg.launch()
+    torch.cuda.synchronize()
+    _check_fused(pairs, shapes)
+    with pytest.raises(nat.GGError, match="SiLU epilogue needs"):  # the large-batch kernel has no WO_SILU tile
+        GroupGemm([pairs[0][1]], variant=names.index("v2x_256x256_w8_b3_buf_spread_edma"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,mode", [(60, "fused"), (2048, "interleaved")])
+def test_moe_ffn_weight_only_fused_equals_unfused(gpu, T, mode):
+    """The reference's small-batch MoE scheme (w4a16 experts beside w8a8, hz_fused.cuh:14-125) with
+    the fused layout: bit-identical to the unfused layer; at T = 60 the gate_up call runs wo3's
+    WO_SILU build, at T = 2048 the large-batch kernel (no weight-only SiLU tile) takes the
+    interleaved form."""
+    topk, E, H, N, Ns = 4, 6, 256, 384, 768
+    g = torch.Generator().manual_seed(23)
+    gate_up = [((torch.rand(2 * N, H, generator=g) * 2 - 1) * 0.2).half() for _ in range(E)]
+    gate_up.append(((torch.rand(2 * Ns, H, generator=g) * 2 - 1) * 0.2).half())
+    down = [((torch.rand(H, N, generator=g) * 2 - 1) * 0.2).half() for _ in range(E)]
+    down.append(((torch.rand(H, Ns, generator=g) * 2 - 1) * 0.2).half())
+    w4a16 = QParams(16, 4, -1, False)
+    qcfg = [(w4a16, w4a16), (W8A8, W8A8), (w4a16, W8A8), (w4a16, w4a16), (QParams(16, 4, 128, True), w4a16),
+            (w4a16, w4a16), (w4a16, w4a16)]
+    gu, dn = [w.to(DEV) for w in gate_up], [w.to(DEV) for w in down]
+    plain = moe.MoEFFN(gu, dn, qcfg, num_routed=E, fuse_silu=False)
+    fused = moe.MoEFFN(gu, dn, qcfg, num_routed=E)
+    assert fused.fuse_silu
+    logits = torch.rand(T, E, generator=g)
+    ids = torch.topk(logits, topk, dim=1).indices.to(torch.int32).to(DEV)
+    wts = torch.softmax(torch.rand(T, topk, generator=g), dim=1).to(DEV)
+    h = ((torch.rand(T, H, generator=g) * 2 - 1) * 3).half().to(DEV)
+    o1, m1 = plain.forward(h, ids, wts, return_intermediates=True)
+    o2, m2 = fused.forward(h, ids, wts, return_intermediates=True)
+    torch.cuda.synchronize()
+    assert torch.equal(m1["a2"].out, m2["a2"].out)
+    assert torch.equal(o1.view(torch.int16), o2.view(torch.int16))
+    assert moe.PlannedForward(fused, h, ids, wts).mode == mode
+
