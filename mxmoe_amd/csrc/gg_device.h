@@ -707,6 +707,20 @@ constexpr int kWoAblMask = ABL_WO_BTILED | ABL_WO_NODMA | ABL_WO_NOCOMPUTE;
 // weight-only problems carry the flag, so the plain 3-WG/CU build keeps its registers (the bit is
 // V2_EPIPE's, a v2 epilogue option no weight-only tile sees)
 constexpr int WO_SILU = 1 << 28;
+// weight-only option (round 6, with WO_SCLATE | WO_SPLIT): a tile whose K stages lie in ONE scale group
+// (per-channel scales — the small-batch bench scheme's w4a16_g-1) runs a loop without the group
+// bookkeeping, unrolled by the ring depth so the ring offsets are constants (the bit is V2_SPREAD's
+// lowest, a v2 option no weight-only tile sees)
+constexpr int WO_PCH = 1 << 18;
+
+// f(integral_constant<int, I>) for I in [I0, N)
+template <int I0, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I0 < N) {
+    f(std::integral_constant<int, I0>());
+    static_for<I0 + 1, N>(f);
+  }
+}
 constexpr int kAblMask = ABL_NO_DMA | ABL_NO_LDS | ABL_NO_EPI | ABL_B_NODMA | ABL_B_REGLOAD | ABL_B_TILED;  // int8-only builds
 
 // Tile timeline (diagnostics, V2_TRACE builds only): per block {start, mainloop end, end (stores
@@ -2622,6 +2636,37 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     static_assert((WABL & WO_SCLATE) == 0 || NBUF * SB_ + NBUF * 1024 <= Cfg::LDSB, "the scale slots sit past the ring");
     uint8_t* const sc_base = lds + NBUF * SB_ + wave * 128;
     load_scales(ks0 / gstages, s2, z2);
+    bool one_group = false;
+    if constexpr ((WABL & WO_PCH) != 0 && (WABL & WO_SPLIT) != 0 && (WABL & WO_ADEAD) == 0)
+      one_group = (ks0 % gstages) + nst <= gstages;
+    if constexpr ((WABL & WO_PCH) != 0 && (WABL & WO_SPLIT) != 0 && (WABL & WO_ADEAD) == 0) {
+     if (one_group) {
+      // WO_PCH: no scale slots, no group counters; the steady loop unrolled by NBUF (ring buffer
+      // s % NBUF a constant in each copy: no per-stage offset arithmetic), the last stages with a
+      // runtime buffer index
+#pragma unroll
+      for (int p = 0; p < DIST; ++p)
+        if (p < nst) issue(p, p);
+      int s = 0;
+      for (; s + NBUF - 1 + DIST < nst; s += NBUF) {
+        static_for<0, NBUF>([&](auto i_c) {
+          constexpr int BC = decltype(i_c)::value;
+          wait_vmcnt<(DIST - 1) * DPS>();
+          lds_barrier();
+          issue(s + BC + DIST, (BC + DIST) % NBUF);
+          if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(BC);
+        });
+      }
+      for (; s < nst; ++s) {
+        if (s + DIST - 1 < nst) wait_vmcnt<(DIST - 1) * DPS>();
+        else wait_stage(nst - 1 - s);
+        lds_barrier();
+        if (s + DIST < nst) issue(s + DIST, (s + DIST) % NBUF);
+        if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF);
+      }
+     }
+    }
+    if (!one_group) {
     const int nl = min(ncol0 + (lane & 31), N - 1);
     int ipos = ks0 % gstages, igrp = ks0 / gstages;  // issue stream: stage t's place in its group
     int cpos = ipos;                                   // compute stream
@@ -2700,6 +2745,7 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
     } else {
       for (int s = 0; s < nst; ++s) step(s, std::true_type());
     }
+    }  // (!one_group)
     wait_vmcnt<0>();
     lds_barrier();  // ring -> epilogue staging
   } else if (nst > 0) {
@@ -2848,7 +2894,7 @@ __global__ __launch_bounds__(512, 2 * NWG) void gg_wo2_kernel(GGArgs args) {
   sk.slabs = args.slabs;
   sk.counters = args.counters;
   typedef WoCfg<64, 1, WO2_LDS_BYTES> Cfg;
-  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | WO_BUF | WO_SILU | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
+  constexpr int WP = ABL & (WO_PIPE | WO_STAG | WO_SCLATE | WO_ANDOR | WO_MSKIP | WO_SPLIT | WO_NIBPOS | WO_ADEAD | WO_BUF | WO_SILU | WO_PCH | kWoAblMask);  // (not V2_TRACE)  // (ablations: lab builds only)
   if ((QM & (1 << QT_I8)) && mt.qtype == QT_I8) {
     // w8a8 beside the weight-only problems (the reference's small-batch w4a16 + w8a8 pairing,
     // hz_fused.cuh:14-125): the plain v2 int8 body on a 64 x 128 tile, 4 x 2 waves of 16 x 64
