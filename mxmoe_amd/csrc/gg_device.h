@@ -2666,7 +2666,74 @@ __device__ __forceinline__ void gg_tile_wo(const GGMeta& mt, const uint8_t* __re
       }
      }
     }
-    if (!one_group) {
+    // WO_PCH, two stages per scale group (g128, the 64-K stages' common group size) from an even
+    // stage: the loop unrolled by lcm(NBUF, 2), so each copy knows its ring buffer AND whether its
+    // stage opens a group (scale slot DMA before the stage's own pieces, as below; slot read after
+    // the barrier) — no group counters
+    // (not for 2-bit codes: their 4-deep ring unrolled 4x spilled the 3-WG/CU build)
+    constexpr bool kTwo = (WABL & WO_PCH) != 0 && (WABL & WO_SPLIT) != 0 && (WABL & WO_ADEAD) == 0 && BITS != 2;
+    bool two_group = false;
+    if constexpr (kTwo) two_group = !one_group && gstages == 2 && (ks0 & 1) == 0;
+    if constexpr (kTwo) {
+     if (two_group) {
+      constexpr int L = NBUF % 2 == 0 ? NBUF : 2 * NBUF;
+      const int nl = min(ncol0 + (lane & 31), N - 1);
+      auto issue_sc2 = [&](int t, int buf) {  // stage t (even, > 0) opens scale group (ks0 + t) / 2
+        if (lane < 32) {
+          const int64_t grp = (ks0 + t) >> 1;
+          if (sym) __builtin_amdgcn_global_load_lds((gbl_void_t*)(SB + grp * N + nl), (lds_void_t*)(sc_base + buf * 1024), 2, 0, 0);
+          else __builtin_amdgcn_global_load_lds((gbl_void_t*)(SB + (grp * N + nl) * 2), (lds_void_t*)(sc_base + buf * 1024), 4, 0, 0);
+        }
+      };
+      auto read_sc = [&](int buf) {
+        const uint8_t* sc = sc_base + buf * 1024;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if (sym) {
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(sc + (j * 16 + r16) * 4);
+            s2[j] = v * 0x10001u;
+            z2[j] = 0;
+          } else {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(sc + (j * 16 + r16) * 4);
+            s2[j] = (v & 0xFFFFu) * 0x10001u;
+            z2[j] = (v >> 16) * 0x10001u;
+          }
+        }
+      };
+#pragma unroll
+      for (int p = 0; p < DIST; ++p)
+        if (p < nst) {
+          if (p > 0 && (p & 1) == 0) issue_sc2(p, p);
+          issue(p, p);
+        }
+      int s = 0;
+      for (; s + L - 1 + DIST < nst; s += L) {
+        static_for<0, L>([&](auto i_c) {
+          constexpr int I = decltype(i_c)::value, BC = I % NBUF, BI = (I + DIST) % NBUF;
+          wait_vmcnt<(DIST - 1) * DPS>();
+          lds_barrier();
+          if constexpr ((I & 1) == 0) {
+            if (I > 0 || s > 0) read_sc(BC);
+          }
+          if constexpr (((I + DIST) & 1) == 0) issue_sc2(s + I + DIST, BI);
+          issue(s + I + DIST, BI);
+          if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(BC);
+        });
+      }
+      for (; s < nst; ++s) {
+        if (s + DIST - 1 < nst) wait_vmcnt<(DIST - 1) * DPS>();
+        else wait_stage(nst - 1 - s);
+        lds_barrier();
+        if (s > 0 && (s & 1) == 0) read_sc(s % NBUF);
+        if (s + DIST < nst) {
+          if (((s + DIST) & 1) == 0) issue_sc2(s + DIST, (s + DIST) % NBUF);
+          issue(s + DIST, (s + DIST) % NBUF);
+        }
+        if constexpr ((WABL & ABL_WO_NOCOMPUTE) == 0) compute(s % NBUF);
+      }
+     }
+    }
+    if (!one_group && !two_group) {
     const int nl = min(ncol0 + (lane & 31), N - 1);
     int ipos = ks0 % gstages, igrp = ks0 / gstages;  // issue stream: stage t's place in its group
     int cpos = ipos;                                   // compute stream

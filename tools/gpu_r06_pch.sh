@@ -13,7 +13,7 @@ V=$(python -c "
 from mxmoe_amd import _native as nat
 n = {l.split()[1]: l.split()[0] for l in nat.list_variants()}
 print(n['x_wo3'] + ',' + n['x_wo3_pch'])")
-for spec in "w4a16_w8a8 512" "w4a16_w8a8 128" "w4a16c 512" "w4a16 512"; do
+for spec in "w4a16_w8a8 512" "w4a16 512" "w4a16 128" "w4a16gs 512" "w4a16c 512"; do
   set -- $spec
   for gg in gate_up down; do
     timeout -k 10 300 python tools/kbench.py --cfg $1 --gg $gg --bs $2 --variants $V --iters 100 --rounds 20 >> $OUT/kbench.jsonl 2>>$OUT/kbench.err || exit 1
