@@ -508,6 +508,7 @@ const std::vector<Variant>& variants() {
       make_wo2<kWo3 | WO_BUF, 3>("x_wo3_buf"),
       make_wo2<kWo3 | WO_ADEAD, 3>("x_wo3_adead"),
       make_wo2<kWo3 | V2_TRACE, 3>("abl_wo3_trace"),
+      make_wo2<kWo3 | WO_PCH | V2_TRACE, 3>("abl_wo3_pch_trace"),  // the product loop, tile timeline
       make_wo2<kWo3 | ABL_WO_NODMA, 3>("abl_wo3_nodma"),
       make_wo2<kWo3 | ABL_WO_NOCOMPUTE, 3>("abl_wo3_nocompute"),
 #else
