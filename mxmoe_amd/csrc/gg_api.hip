@@ -246,8 +246,9 @@ void launch_wo2(const GGArgs& a, int grid, int qmask, hipStream_t s) {
   if (qmask & kQmaskWoSilu) {  // weight-only problems with the fused SiLU epilogue (WO_SILU builds)
     constexpr int AS = ABL | WO_SILU;
     switch (qmask & 511) {
-      case 8: launch_wo2_q<AS, 8, NWG>(a, grid, s); break;    // w4a16 (+ fp16 / w8a8 / w4a4 riding along
-      case 10: launch_wo2_q<AS, 10, NWG>(a, grid, s); break;  // take the wide build below)
+      case 8: launch_wo2_q<AS, 8, NWG>(a, grid, s); break;    // w4a16
+      case 10: launch_wo2_q<AS, 10, NWG>(a, grid, s); break;  // w4a16 + w8a8 (any other mix: the wide
+                                                              // 2-WG/CU builds below)
       case 16: launch_wo2_q<AS, 16, 2>(a, grid, s); break;
       default: launch_wo2_q<AS, 95, 2>(a, grid, s); break;
     }
@@ -449,7 +450,7 @@ typedef TileCfg<128, 256, 2, 2, 1> T128x256;
 // the fused SiLU epilogue (MXMOE_GG_EPI_SILU_MUL) lives in the fp16 / w8a8 / w4a4 tile bodies of the
 // v2 / v3 kernels (gg_tile_v2, epilogue_v3) — the small-batch wo3 kernel's 64 x 128 bodies of those
 // types included (round 6); the persistent, v4d and fp6 lab kernels have none (mxmoe_gg_variant_caps
-// reports it). Weight-only problems never carry the flag (build_meta).
+// reports it). Weight-only problems may carry the flag on wo3 only (Variant::silu_wo, build_meta).
 bool has_silu_epilogue(const Variant& v) { return v.silu_epi && !v.persistent; }
 
 // Production variants (libmxmoe_gg.so): every one computes correct results. The lab build
