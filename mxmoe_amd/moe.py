@@ -451,7 +451,7 @@ class MoEFFN:
         self.qcfg = list(qcfg)
         eligible = all(q[0].qcfg in self.FUSE_QCFGS or (self.FUSE_WEIGHT_ONLY and q[0].is_weight_only) for q in qcfg)
         if fuse_silu and not eligible:
-            raise ValueError(f"fuse_silu needs every gate_up qcfg in {self.FUSE_QCFGS}")
+            raise ValueError(f"fuse_silu needs every gate_up qcfg in {self.FUSE_QCFGS} or weight-only")
         self.fuse_silu = eligible if fuse_silu is None else fuse_silu
         self.w1 = [prepare_weight(w, q[0], interleave=self.fuse_silu) for w, q in zip(gate_up, qcfg)]
         self.w2 = [prepare_weight(w, q[1]) for w, q in zip(down, qcfg)]
@@ -483,6 +483,8 @@ class MoEFFN:
                           mode == "fused")
             return ps, h1, h1s
 
+        if self.gate_up_mode not in (None, "interleaved"):
+            raise ValueError(f"gate_up_mode must be None or 'interleaved', got {self.gate_up_mode!r}")
         mode = "plain"
         if self.fuse_silu and self.gate_up_mode == "interleaved":
             mode = "interleaved"
