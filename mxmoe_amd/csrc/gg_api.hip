@@ -1237,7 +1237,8 @@ int plan_host(const std::vector<HostProblem>& probs, int variant, bool check_ptr
       len = std::min(64, (rem + nc - 1) / nc);
     }
     const int s1 = std::min(TS, s0 + len);
-    double times[64];
+    // (a chunk can be a whole XCD's slots: 96 for the 3-WG/CU kernel — sized per chunk, not fixed)
+    std::vector<double> times(std::max(0, s1 - s0));
     for (int s = s0; s < s1; ++s) times[s - s0] = tile_time(seq[s]);
     int best = c % 8;
     if (!round_robin && head) {  // full chunks: least total time (cheap; the tail evens out)

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -229,3 +230,35 @@ def test_tail_chunks_scatter_split_slices_across_xcds(wa, K):
     shapes = [QShape([128, 2048, K], *wa), QShape([40, 256, 1408], *wa)]
     tiles, _, _ = check_coverage(shapes)
     assert cross_xcd_split_groups(tiles) > 0
+
+
+def test_lab_planner_knobs_plan_the_small_batch_kernel():
+    """The lab library's planner A/B switches on the 3-WG/CU small-batch kernel, whose XCD chunk is 96
+    slots: plain round-robin or unaligned chunks take a whole chunk at once (a fixed 64-entry buffer
+    overflowed there until round 6). Runs the lab library in a subprocess (CPU: planning only); skips
+    when the lab library is absent or older than its sources."""
+    import subprocess
+    import sys
+
+    from mxmoe_amd import build
+
+    if not build.LAB_LIB.exists() or build.needs_build(build.LAB_LIB):
+        pytest.skip("lab library absent or stale")
+    code = (
+        "import numpy as np\n"
+        "from mxmoe_amd import _native as nat\n"
+        "from mxmoe_amd.workload import load_workload, qwen2_layer11_workload, w4a16_w8a8_qconfig\n"
+        "from tests.test_planner import _probs\n"
+        "names = [l.split()[1] for l in nat.list_variants()]\n"
+        "v = names.index('x_wo3_pch')\n"
+        "for gg in ('gate_up', 'down'):\n"
+        "    probs = _probs(load_workload(qwen2_layer11_workload(512, qconfig=w4a16_w8a8_qconfig()))['layer-11'][gg])\n"
+        "    tiles, rows = nat.plan_tiles(probs, v)\n"
+        "    assert (tiles[:, 0] >= 0).sum() > 0\n"
+        "print('ok')\n")
+    for knob in ("MXMOE_GG_XCD_RR=1", "MXMOE_GG_ALIGN=0", "MXMOE_GG_TAIL_CHUNK=96"):
+        k, val = knob.split("=")
+        env = dict(os.environ, MXMOE_GG_LIB=str(build.LAB_LIB), **{k: val})
+        r = subprocess.run([sys.executable, "-c", code], cwd=str(build.ROOT),
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "ok" in r.stdout, (knob, r.returncode, r.stderr[-800:])
